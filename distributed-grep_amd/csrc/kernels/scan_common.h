@@ -1,0 +1,43 @@
+// scan_common.h — types shared by the scan kernels and the host runtime.
+#pragma once
+#include <stdint.h>
+
+namespace dgrep {
+
+// One matching line as produced by a tile, before global ordering.
+// `rel` = number of '\n' between the tile start and the line start, so the
+// 1-based line number (application/grep.go:25 `line_number+1`) is
+// newlines_before_tile + rel + 1.
+struct StagedLine {
+  uint64_t start;  // absolute byte offset of the line in the split
+  uint32_t len;    // bytes, '\n' excluded
+  uint32_t rel;
+};
+
+// Per-tile bookkeeping written by the scan kernel.
+struct TileInfo {
+  uint64_t base;   // first StagedLine of this tile in the staging buffer
+  uint32_t count;  // matching lines owned by the tile
+  uint32_t nl;     // '\n' bytes inside the tile
+};
+
+struct ScanArgs {
+  const uint8_t* data;
+  uint64_t n;
+  const uint8_t* table;   // u8 transition table, [state][byte] (nstates*256 bytes)
+  uint32_t table_bytes;
+  uint32_t start, start_m;
+  uint32_t pad;
+  uint64_t ntiles;
+  StagedLine* staging;
+  uint64_t capacity;      // staging/output capacity in lines
+  unsigned long long* counter;  // staging append counter
+  TileInfo* tiles;
+  uint32_t* status;       // error bits (kStatus*)
+};
+
+enum : uint32_t { kStatusLineTooLong = 1u };
+
+constexpr int kScanThreads = 256;
+
+}  // namespace dgrep

@@ -1,0 +1,365 @@
+// dgrep_runtime.hip — device contexts, DFA upload, split scanning (C ABI).
+//
+// This is the native runtime under the grep plugin's Map (application/grep.go:13-36):
+// dgrep_scan replaces the strings.Split + per-line regexp.Match loop
+// (grep.go:17-29) for one split. Everything here is fail-stop: a HIP error is
+// returned as DGREP_E_HIP with its message in dgrep_last_error; there is no
+// CPU fallback path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/dgrep.h"
+#include "../../../include/dgrep_blob.h"
+#include "../kernels/scan_common.h"
+#include "../kernels/synth.h"
+
+namespace dgrep {
+// scan_dfa.hip
+uint64_t scan_tile_bytes();
+size_t scan_dfa8_lds_bytes(uint32_t table_bytes);
+hipError_t scan_dfa8_occupancy(uint32_t table_bytes, int* blocks_per_cu);
+hipError_t scan_dfa8(const ScanArgs& a, int grid, hipStream_t stream);
+hipError_t tile_scan(TileInfo* tiles, uint64_t ntiles, uint64_t* out_off, uint64_t* line_base, hipStream_t stream);
+hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, const uint64_t* out_off,
+                       const uint64_t* line_base, uint64_t capacity, uint64_t* line_no, uint64_t* start,
+                       uint32_t* len, hipStream_t stream);
+}  // namespace dgrep
+
+using namespace dgrep;
+
+struct dgrep_ctx {
+  int device = 0;
+  int num_cus = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // loaded pattern
+  bool loaded = false;
+  uint32_t flags = 0, nstates = 0, start = 0, start_m = 0;
+  bool empty_line_matches = false;
+  uint8_t* d_table = nullptr;  // u8 [state][byte]
+  uint32_t table_bytes = 0;
+  int blocks_per_cu = 1;
+
+  // per-scan scratch (grown on demand, reused)
+  TileInfo* d_tiles = nullptr;
+  uint64_t* d_out_off = nullptr;
+  uint64_t* d_line_base = nullptr;
+  uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0;
+  StagedLine* d_staging = nullptr;
+  uint64_t staging_cap = 0;
+  unsigned long long* d_counter = nullptr;
+  uint32_t* d_status = nullptr;
+
+  // dgrep_scan (host data) buffers
+  uint8_t* d_data = nullptr;
+  size_t data_cap = 0;
+  uint64_t* d_res_line = nullptr;
+  uint64_t* d_res_start = nullptr;
+  uint32_t* d_res_len = nullptr;
+  uint64_t res_cap = 0;
+
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_ms = 0.f;
+};
+
+namespace {
+
+int hip_fail(dgrep_ctx* c, hipError_t e, const char* what) {
+  c->err = std::string(what) + ": " + hipGetErrorString(e);
+  return DGREP_E_HIP;
+}
+#define HIPCHK(expr)                                   \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(c, e_, #expr); \
+  } while (0)
+
+template <class T>
+int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
+  if (*cap >= need && *p) return DGREP_OK;
+  if (*p) HIPCHK(hipFree(*p));
+  *p = nullptr;
+  uint64_t n = std::max<uint64_t>(need, 1);
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)));
+  *cap = n;
+  return DGREP_OK;
+}
+
+}  // namespace
+
+extern "C" int dgrep_open(int device, dgrep_ctx** out) {
+  if (!out) return DGREP_E_INVALID;
+  *out = nullptr;
+  dgrep_ctx* c = new dgrep_ctx();
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_counter), sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_status), sizeof(uint32_t));
+  if (e != hipSuccess) {
+    // keep the context so the caller can read the message
+    c->err = std::string("dgrep_open: ") + hipGetErrorString(e);
+    *out = c;
+    return DGREP_E_HIP;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return DGREP_OK;
+}
+
+extern "C" void dgrep_close(dgrep_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->d_table, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counter,
+                  c->d_status, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+extern "C" const char* dgrep_last_error(dgrep_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int dgrep_set_stream(dgrep_ctx* c, void* s) {
+  if (!c) return DGREP_E_INVALID;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
+  if (!c) return DGREP_E_INVALID;
+  dgrep_blob_info info;
+  if (dgrep_blob_info_get(blob, n, &info) != DGREP_OK) {
+    c->err = "dgrep_load_dfa: malformed blob";
+    return DGREP_E_INVALID;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  dgrep_blob_header h;
+  memcpy(&h, blob, sizeof h);
+  const uint32_t* trans = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(blob) + sizeof h);
+  for (size_t i = 0; i < size_t(h.nstates) * h.nclasses; ++i)
+    if (trans[i] >= h.nstates) {
+      c->err = "dgrep_load_dfa: transition out of range";
+      return DGREP_E_INVALID;
+    }
+  if (h.nstates > 256) {
+    c->err = "dgrep_load_dfa: DFA has " + std::to_string(h.nstates) +
+             " states; this build scans DFAs of at most 256 states (LDS-resident u8 table)";
+    return DGREP_E_UNSUPPORTED;
+  }
+  // expand byte classes: table[s*256 + b] = trans[s][class(b)]
+  std::vector<uint8_t> t(size_t(h.nstates) * 256);
+  for (uint32_t s = 0; s < h.nstates; ++s)
+    for (int b = 0; b < 256; ++b) t[size_t(s) * 256 + size_t(b)] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
+  if (c->d_table) HIPCHK(hipFree(c->d_table));
+  c->d_table = nullptr;
+  c->table_bytes = uint32_t(t.size());
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_table), (t.size() + 15) & ~size_t(15)));
+  HIPCHK(hipMemcpy(c->d_table, t.data(), t.size(), hipMemcpyHostToDevice));
+  c->flags = h.flags;
+  c->nstates = h.nstates;
+  c->start = h.start;
+  c->start_m = h.start_m;
+  c->empty_line_matches = trans[size_t(h.start) * h.nclasses + h.byte_class[uint8_t('\n')]] == h.start_m;
+  int bpc = 0;
+  HIPCHK(scan_dfa8_occupancy(c->table_bytes, &bpc));
+  c->blocks_per_cu = std::max(1, bpc);
+  c->loaded = true;
+  return DGREP_OK;
+}
+
+// Core of every scan: the split is resident at d_data (n bytes). Results go to
+// device arrays of `capacity` lines; *count receives the number of matches.
+static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64_t* d_line, uint64_t* d_start,
+                         uint32_t* d_len, uint64_t capacity, uint64_t* count) {
+  *count = 0;
+  if (c->flags & DGREP_DFA_MATCH_NONE) return DGREP_OK;
+  if (n == 0) {
+    // strings.Split("", "\n") == [""]: one empty line, line 1
+    if (!c->empty_line_matches) return DGREP_OK;
+    *count = 1;
+    if (capacity >= 1) {
+      const uint64_t one = 1, zero = 0;
+      const uint32_t zl = 0;
+      HIPCHK(hipMemcpyAsync(d_line, &one, 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(d_start, &zero, 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(d_len, &zl, 4, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return DGREP_OK;
+  }
+  if (reinterpret_cast<uintptr_t>(d_data) & 15) {
+    c->err = "device split must be 16-byte aligned";
+    return DGREP_E_INVALID;
+  }
+  const uint64_t tile = scan_tile_bytes();
+  const uint64_t ntiles = (n + tile - 1) / tile;
+  int rc;
+  if ((rc = grow(c, &c->d_tiles, &c->tiles_cap, ntiles)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_out_off, &c->off_cap, ntiles + 1)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_line_base, &c->lb_cap, ntiles + 1)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_staging, &c->staging_cap, capacity)) != DGREP_OK) return rc;
+
+  ScanArgs a;
+  memset(&a, 0, sizeof a);
+  a.data = d_data;
+  a.n = n;
+  a.table = c->d_table;
+  a.table_bytes = c->table_bytes;
+  a.start = c->start;
+  a.start_m = c->start_m;
+  a.ntiles = ntiles;
+  a.staging = c->d_staging;
+  a.capacity = capacity;
+  a.counter = c->d_counter;
+  a.tiles = c->d_tiles;
+  a.status = c->d_status;
+  HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_status, 0, 4, c->stream));
+  const uint64_t resident = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
+  const int grid = int(std::min<uint64_t>(ntiles, resident));
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  HIPCHK(scan_dfa8(a, grid, c->stream));
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  unsigned long long total = 0;
+  uint32_t status = 0;
+  HIPCHK(hipMemcpyAsync(&total, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(&status, c->d_status, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  if (status & kStatusLineTooLong) {
+    c->err = "a matching line is longer than 4 GiB (uint32 length in dgrep_result)";
+    return DGREP_E_UNSUPPORTED;
+  }
+  *count = total;
+  if (total == 0 || total > capacity) return DGREP_OK;
+  HIPCHK(tile_scan(c->d_tiles, ntiles, c->d_out_off, c->d_line_base, c->stream));
+  HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, capacity, d_line, d_start, d_len,
+                     c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_scan_device(dgrep_ctx* c, const void* d_data, size_t n, uint64_t* d_line_no, uint64_t* d_start,
+                                 uint32_t* d_len, uint64_t capacity, uint64_t* count) {
+  if (!c || !count || (n && !d_data)) return DGREP_E_INVALID;
+  if (!c->loaded) { c->err = "no DFA loaded"; return DGREP_E_NO_DFA; }
+  HIPCHK(hipSetDevice(c->device));
+  return scan_resident(c, static_cast<const uint8_t*>(d_data), n, d_line_no, d_start, d_len, capacity, count);
+}
+
+extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_result* out) {
+  if (!c || !out || (n && !data)) return DGREP_E_INVALID;
+  memset(out, 0, sizeof *out);
+  if (!c->loaded) { c->err = "no DFA loaded"; return DGREP_E_NO_DFA; }
+  HIPCHK(hipSetDevice(c->device));
+  int rc;
+  if (n) {
+    uint64_t cap = c->data_cap;
+    if ((rc = grow(c, &c->d_data, &cap, (n + 63) & ~uint64_t(63))) != DGREP_OK) return rc;
+    c->data_cap = cap;
+    HIPCHK(hipMemcpyAsync(c->d_data, data, n, hipMemcpyHostToDevice, c->stream));
+  }
+  uint64_t want = std::max<uint64_t>(c->res_cap, std::max<uint64_t>(1024, n / 512));
+  uint64_t count = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (want > c->res_cap) {
+      uint64_t c1 = 0, c2 = 0, c3 = 0;
+      if (c->d_res_line) { HIPCHK(hipFree(c->d_res_line)); c->d_res_line = nullptr; }
+      if (c->d_res_start) { HIPCHK(hipFree(c->d_res_start)); c->d_res_start = nullptr; }
+      if (c->d_res_len) { HIPCHK(hipFree(c->d_res_len)); c->d_res_len = nullptr; }
+      if ((rc = grow(c, &c->d_res_line, &c1, want)) != DGREP_OK) return rc;
+      if ((rc = grow(c, &c->d_res_start, &c2, want)) != DGREP_OK) return rc;
+      if ((rc = grow(c, &c->d_res_len, &c3, want)) != DGREP_OK) return rc;
+      c->res_cap = want;
+    }
+    if ((rc = scan_resident(c, c->d_data, n, c->d_res_line, c->d_res_start, c->d_res_len, c->res_cap, &count)) !=
+        DGREP_OK)
+      return rc;
+    if (count <= c->res_cap) break;
+    want = count;
+  }
+  out->count = count;
+  if (count == 0) return DGREP_OK;
+  out->line_no = static_cast<uint64_t*>(malloc(count * 8));
+  out->start = static_cast<uint64_t*>(malloc(count * 8));
+  out->len = static_cast<uint32_t*>(malloc(count * 4));
+  if (!out->line_no || !out->start || !out->len) {
+    dgrep_result_free(out);
+    return DGREP_E_NOMEM;
+  }
+  HIPCHK(hipMemcpyAsync(out->line_no, c->d_res_line, count * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out->start, c->d_res_start, count * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out->len, c->d_res_len, count * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return DGREP_OK;
+}
+
+extern "C" void dgrep_result_free(dgrep_result* r) {
+  if (!r) return;
+  free(r->line_no);
+  free(r->start);
+  free(r->len);
+  memset(r, 0, sizeof *r);
+}
+
+extern "C" int dgrep_last_kernel_ms(dgrep_ctx* c, float* ms) {
+  if (!c || !ms) return DGREP_E_INVALID;
+  *ms = c->last_ms;
+  return DGREP_OK;
+}
+
+// ---- synthetic corpus ------------------------------------------------------
+__global__ void synth_kernel(char* out, uint64_t n, uint64_t seed, int kind) {
+  const uint64_t pages = (n + synth::kPage - 1) / synth::kPage;
+  for (uint64_t p = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < pages; p += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t off = p * synth::kPage;
+    const uint32_t bytes = uint32_t(std::min<uint64_t>(synth::kPage, n - off));
+    synth::page_fill(seed, p, kind, out + off, bytes);
+  }
+}
+
+extern "C" int dgrep_synth_corpus(dgrep_ctx* c, void* d_out, size_t n, uint64_t seed, int kind) {
+  if (!c || (n && !d_out)) return DGREP_E_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  if (n == 0) return DGREP_OK;
+  const uint64_t pages = (n + synth::kPage - 1) / synth::kPage;
+  const int block = 256;
+  const int grid = int(std::min<uint64_t>((pages + block - 1) / block, 65536));
+  hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(block), 0, c->stream, static_cast<char*>(d_out), uint64_t(n),
+                     seed, kind);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return DGREP_OK;
+}
+
+// Host twin of dgrep_synth_corpus (same code path, synth.h): used by tests to
+// regenerate any window of a device corpus on the CPU.
+extern "C" int dgrep_synth_corpus_host(void* out, size_t n, uint64_t seed, int kind) {
+  if (n && !out) return DGREP_E_INVALID;
+  const uint64_t pages = (n + synth::kPage - 1) / synth::kPage;
+  for (uint64_t p = 0; p < pages; ++p) {
+    const uint64_t off = p * synth::kPage;
+    const uint32_t bytes = uint32_t(std::min<uint64_t>(synth::kPage, n - off));
+    synth::page_fill(seed, p, kind, static_cast<char*>(out) + off, bytes);
+  }
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_synth_keyword(uint64_t seed, int i, char* out16) {
+  if (!out16 || i < 0 || i >= synth::kKeywords) return -1;
+  return synth::keyword(seed, i, out16);
+}

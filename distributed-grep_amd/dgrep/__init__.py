@@ -1,0 +1,309 @@
+"""dgrep — host-side mirror of distributed-grep's grep plugin over libdgrep.so.
+
+The reference plugin (application/grep.go) exports
+
+    func Map(filename string, contents string) []mapreduce.KeyValue   // grep.go:13-36
+    func Reduce(key string, values []string) string                   // grep.go:38-40
+
+with the pattern held in the package variable `pattern` (grep.go:11, default
+""). This module keeps those names, argument meanings and error behaviour:
+
+* ``Map(filename, contents)`` returns ``[KeyValue(Key, Value), ...]`` in line
+  order, Key = ``"%s (line number #%d)" % (filename, n)`` (grep.go:25), Value =
+  the line without its '\\n'. A pattern that Go's regexp.Compile rejects gives
+  an empty list (grep.go:21 discards the error). Any device failure raises
+  (the Go plugin would panic, and the coordinator re-assigns the task after
+  its 10 s timeout, map_reduce/coordinator.go:105).
+* ``Reduce(key, values)`` returns ``values[0]``.
+* ``pattern`` defaults to "" (every line matches) and can be overridden with
+  the DGREP_PATTERN environment variable or :func:`set_pattern`.
+
+The matching itself runs on the GPU through the C ABI in include/dgrep.h; there
+is no CPU fallback: if libdgrep.so or a GPU is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from collections import namedtuple
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdgrep.so")
+
+DGREP_OK = 0
+DGREP_E_INVALID = 1
+DGREP_E_UNSUPPORTED = 2
+DGREP_E_TOO_LARGE = 3
+DGREP_E_HIP = 4
+DGREP_E_NOMEM = 5
+DGREP_E_NO_DFA = 6
+
+DFA_GO_SYNTAX_ERROR = 1
+DFA_MATCH_NONE = 2
+DFA_MATCH_ALL = 4
+
+# Symbols declared in include/dgrep.h (tests check the library exports all).
+EXPORTS = (
+    "dgrep_compile", "dgrep_blob_free", "dgrep_blob_info_get", "dgrep_open", "dgrep_close",
+    "dgrep_last_error", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
+    "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
+    "dgrep_last_kernel_ms",
+)
+
+KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
+
+
+class DgrepError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("dgrep error %d: %s" % (code, msg))
+        self.code = code
+
+
+class UnsupportedPattern(DgrepError):
+    pass
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64), ("line_no", ctypes.POINTER(ctypes.c_uint64)),
+                ("start", ctypes.POINTER(ctypes.c_uint64)), ("len", ctypes.POINTER(ctypes.c_uint32))]
+
+
+class _BlobInfo(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint32), ("nstates", ctypes.c_uint32), ("nclasses", ctypes.c_uint32),
+                ("start", ctypes.c_uint32), ("start_m", ctypes.c_uint32)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    """Load libdgrep.so (fails loudly if it was not built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError("libdgrep.so not built (run __graft_entry__.build() or `make`): " + LIB_PATH)
+            L = ctypes.CDLL(LIB_PATH)
+            vp, sz, u64, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
+            L.dgrep_compile.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.c_char_p, sz]
+            L.dgrep_compile.restype = i
+            L.dgrep_blob_free.argtypes = [vp]
+            L.dgrep_blob_free.restype = None
+            L.dgrep_blob_info_get.argtypes = [vp, sz, ctypes.POINTER(_BlobInfo)]
+            L.dgrep_blob_info_get.restype = i
+            L.dgrep_open.argtypes = [i, ctypes.POINTER(vp)]
+            L.dgrep_open.restype = i
+            L.dgrep_close.argtypes = [vp]
+            L.dgrep_close.restype = None
+            L.dgrep_last_error.argtypes = [vp]
+            L.dgrep_last_error.restype = ctypes.c_char_p
+            L.dgrep_set_stream.argtypes = [vp, vp]
+            L.dgrep_set_stream.restype = i
+            L.dgrep_load_dfa.argtypes = [vp, vp, sz]
+            L.dgrep_load_dfa.restype = i
+            L.dgrep_scan.argtypes = [vp, vp, sz, ctypes.POINTER(_Result)]
+            L.dgrep_scan.restype = i
+            L.dgrep_result_free.argtypes = [ctypes.POINTER(_Result)]
+            L.dgrep_result_free.restype = None
+            L.dgrep_scan_device.argtypes = [vp, vp, sz, vp, vp, vp, u64, ctypes.POINTER(u64)]
+            L.dgrep_scan_device.restype = i
+            L.dgrep_synth_corpus.argtypes = [vp, vp, sz, u64, i]
+            L.dgrep_synth_corpus.restype = i
+            L.dgrep_synth_corpus_host.argtypes = [vp, sz, u64, i]
+            L.dgrep_synth_corpus_host.restype = i
+            L.dgrep_synth_keyword.argtypes = [u64, i, ctypes.c_char_p]
+            L.dgrep_synth_keyword.restype = i
+            L.dgrep_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+            L.dgrep_last_kernel_ms.restype = i
+            _lib = L
+    return _lib
+
+
+class CompiledPattern:
+    """A pattern compiled by dgrep_compile (Go regexp/syntax semantics)."""
+
+    def __init__(self, pattern):
+        if isinstance(pattern, str):
+            pattern = pattern.encode("utf-8", "surrogateescape")
+        self.pattern = bytes(pattern)
+        L = lib()
+        blob = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        err = ctypes.create_string_buffer(512)
+        rc = L.dgrep_compile(self.pattern, len(self.pattern), ctypes.byref(blob), ctypes.byref(n), err, 512)
+        msg = err.value.decode(errors="replace")
+        if rc == DGREP_E_UNSUPPORTED:
+            raise UnsupportedPattern(rc, msg)
+        if rc != DGREP_OK:
+            raise DgrepError(rc, msg)
+        self.blob = ctypes.string_at(blob, n.value)
+        L.dgrep_blob_free(blob)
+        info = _BlobInfo()
+        rc = L.dgrep_blob_info_get(self.blob, len(self.blob), ctypes.byref(info))
+        if rc != DGREP_OK:
+            raise DgrepError(rc, "malformed blob")
+        self.flags = info.flags
+        self.nstates = info.nstates
+        self.nclasses = info.nclasses
+        self.start = info.start
+        self.start_m = info.start_m
+        self.message = msg
+
+    @property
+    def go_syntax_error(self) -> bool:
+        return bool(self.flags & DFA_GO_SYNTAX_ERROR)
+
+    def tables(self) -> Tuple[np.ndarray, np.ndarray]:
+        """(byte_class[256] u8, trans[nstates, nclasses] u32) — for tests/inspection."""
+        bc = np.frombuffer(self.blob[32:288], dtype=np.uint8)
+        tr = np.frombuffer(self.blob[288:], dtype=np.uint32).reshape(self.nstates, self.nclasses)
+        return bc, tr
+
+
+class Context:
+    """One device context (a HIP device + stream) — dgrep_open/close."""
+
+    def __init__(self, device: int = 0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        rc = self._L.dgrep_open(device, ctypes.byref(h))
+        self._h = h
+        if rc != DGREP_OK:
+            msg = self._err()
+            self.close()
+            raise DgrepError(rc, msg)
+        self.device = device
+        self.pattern: Optional[CompiledPattern] = None
+
+    def _err(self) -> str:
+        m = self._L.dgrep_last_error(self._h)
+        return m.decode(errors="replace") if m else ""
+
+    def _check(self, rc: int):
+        if rc != DGREP_OK:
+            if rc == DGREP_E_UNSUPPORTED:
+                raise UnsupportedPattern(rc, self._err())
+            raise DgrepError(rc, self._err())
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.dgrep_close(self._h)
+        self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, hip_stream: int):
+        self._check(self._L.dgrep_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
+    def load(self, pattern) -> CompiledPattern:
+        cp = pattern if isinstance(pattern, CompiledPattern) else CompiledPattern(pattern)
+        self._check(self._L.dgrep_load_dfa(self._h, cp.blob, len(cp.blob)))
+        self.pattern = cp
+        return cp
+
+    def scan(self, contents) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Host split -> (line_no u64[], start u64[], len u32[]) of matching lines."""
+        if isinstance(contents, str):
+            contents = contents.encode("utf-8", "surrogateescape")
+        buf = np.frombuffer(contents, dtype=np.uint8) if len(contents) else np.zeros(1, np.uint8)
+        res = _Result()
+        self._check(self._L.dgrep_scan(self._h, ctypes.c_void_p(buf.ctypes.data), len(contents), ctypes.byref(res)))
+        try:
+            n = int(res.count)
+            if n == 0:
+                return np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint32)
+            ln = np.ctypeslib.as_array(res.line_no, shape=(n,)).copy()
+            st = np.ctypeslib.as_array(res.start, shape=(n,)).copy()
+            le = np.ctypeslib.as_array(res.len, shape=(n,)).copy()
+            return ln, st, le
+        finally:
+            self._L.dgrep_result_free(ctypes.byref(res))
+
+    def scan_device(self, d_data: int, n: int, d_line: int, d_start: int, d_len: int, capacity: int) -> int:
+        """HBM-resident split at device pointer d_data; returns the match count."""
+        cnt = ctypes.c_uint64()
+        self._check(self._L.dgrep_scan_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(d_line),
+                                              ctypes.c_void_p(d_start), ctypes.c_void_p(d_len), capacity,
+                                              ctypes.byref(cnt)))
+        return int(cnt.value)
+
+    def synth(self, d_out: int, n: int, seed: int, kind: int = 0):
+        self._check(self._L.dgrep_synth_corpus(self._h, ctypes.c_void_p(d_out), n, seed, kind))
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float()
+        self._check(self._L.dgrep_last_kernel_ms(self._h, ctypes.byref(ms)))
+        return float(ms.value)
+
+
+def synth_corpus_host(n: int, seed: int, kind: int = 0) -> bytes:
+    """CPU twin of dgrep_synth_corpus (same generator code, synth.h)."""
+    out = ctypes.create_string_buffer(max(n, 1))
+    rc = lib().dgrep_synth_corpus_host(out, n, seed, kind)
+    if rc != DGREP_OK:
+        raise DgrepError(rc, "synth")
+    return out.raw[:n]
+
+
+def synth_keywords(seed: int, count: int = 1000) -> List[bytes]:
+    out = []
+    buf = ctypes.create_string_buffer(16)
+    for i in range(count):
+        k = lib().dgrep_synth_keyword(seed, i, buf)
+        out.append(buf.raw[:k])
+    return out
+
+
+# ---- the plugin surface (application/grep.go) --------------------------------
+
+pattern: str = os.environ.get("DGREP_PATTERN", "")  # grep.go:11 `var pattern string = ""`
+
+_ctx_local = threading.local()
+
+
+def set_pattern(p: str):
+    global pattern
+    pattern = p
+
+
+def _context() -> Context:
+    ctx = getattr(_ctx_local, "ctx", None)
+    if ctx is None:
+        ctx = Context(int(os.environ.get("DGREP_DEVICE", "0")))
+        _ctx_local.ctx = ctx
+        _ctx_local.loaded = None
+    if _ctx_local.loaded != pattern:
+        ctx.load(pattern)
+        _ctx_local.loaded = pattern
+    return ctx
+
+
+def format_key(filename: str, line_no: int) -> str:
+    """fmt.Sprintf("%s (line number #%v)", filename, line_number+1) (grep.go:25)."""
+    return "%s (line number #%d)" % (filename, line_no)
+
+
+def Map(filename: str, contents) -> List[KeyValue]:
+    """grep.go:13-36 on the GPU: matching lines of `contents`, in line order."""
+    raw = contents.encode("utf-8", "surrogateescape") if isinstance(contents, str) else bytes(contents)
+    ln, st, le = _context().scan(raw)
+    kva = []
+    for n, s, l in zip(ln.tolist(), st.tolist(), le.tolist()):
+        v = raw[s:s + l]
+        kva.append(KeyValue(format_key(filename, n), v.decode("utf-8", "surrogateescape")
+                            if isinstance(contents, str) else v))
+    return kva
+
+
+def Reduce(key: str, values: Sequence[str]) -> str:
+    """grep.go:38-40."""
+    return values[0]

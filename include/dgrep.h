@@ -1,0 +1,123 @@
+/*
+ * dgrep.h — C ABI of libdgrep.so, the MI355X-native Map hot path of
+ * distributed-grep (bgilby59/distributed-grep).
+ *
+ * The reference path being replaced is the body of the grep plugin's Map:
+ *
+ *   application/grep.go:13-36
+ *     lines := strings.Split(contents, "\n")                 // grep.go:17
+ *     for line_number, line := range lines {                 // grep.go:20
+ *         matched, _ := regexp.Match(pattern, []byte(line))  // grep.go:21
+ *         if matched {                                       // grep.go:24-29
+ *             k := fmt.Sprintf("%s (line number #%v)", filename, line_number+1)
+ *             kva = append(kva, KeyValue{Key: k, Value: line})
+ *
+ * A cgo-built Map binds exactly these entry points: it
+ * compiles `pattern` once (dgrep_compile -> dgrep_load_dfa, replacing the
+ * per-line regexp.Compile inside regexp.Match at grep.go:21), scans the split
+ * on the GPU (dgrep_scan, replacing grep.go:17-24), and rebuilds each
+ * KeyValue on the host from (line_no, start, len): Key = Sprintf(filename,
+ * line_no), Value = contents[start:start+len] (grep.go:25-28). Reduce
+ * (grep.go:38-40) is unchanged.
+ *
+ * Conventions: every function returns an int status (DGREP_OK = 0). The
+ * library borrows `data` only for the duration of a call; result arrays are
+ * owned by the library until dgrep_result_free. Each entry point sets the
+ * context's HIP device, so a Go goroutine may migrate between OS threads.
+ * One context per device stream; contexts share no mutable state.
+ */
+#ifndef DGREP_H
+#define DGREP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  DGREP_OK = 0,
+  DGREP_E_INVALID = 1,     /* bad argument / malformed blob */
+  DGREP_E_UNSUPPORTED = 2, /* valid Go regexp outside the compiler's subset: refuse, never guess */
+  DGREP_E_TOO_LARGE = 3,   /* automaton exceeds the compiler's state budget */
+  DGREP_E_HIP = 4,         /* HIP runtime error (message in dgrep_last_error) */
+  DGREP_E_NOMEM = 5,
+  DGREP_E_NO_DFA = 6,      /* scan before dgrep_load_dfa */
+};
+
+/* Flags carried in a compiled blob (dgrep_blob_info). */
+enum {
+  DGREP_DFA_GO_SYNTAX_ERROR = 1u << 0, /* Go's regexp.Compile rejects the pattern: no line matches (grep.go:21 drops err) */
+  DGREP_DFA_MATCH_NONE = 1u << 1,      /* no line can match */
+  DGREP_DFA_MATCH_ALL = 1u << 2,       /* every line matches (e.g. the shipped pattern "" at grep.go:11) */
+};
+
+typedef struct dgrep_ctx dgrep_ctx;
+
+/* Matching lines of one split, ascending line order (grep.go:20 iteration
+ * order). line_no is 1-based (grep.go:25 `line_number+1`); start/len index
+ * the split's bytes; the line excludes its '\n' (strings.Split). */
+typedef struct {
+  uint64_t count;
+  uint64_t* line_no;
+  uint64_t* start;
+  uint32_t* len;
+} dgrep_result;
+
+typedef struct {
+  uint32_t flags;
+  uint32_t nstates;  /* minimized DFA states */
+  uint32_t nclasses; /* byte equivalence classes */
+  uint32_t start;
+  uint32_t start_m;  /* the state entered by a '\n' that ends a matching line */
+} dgrep_blob_info;
+
+/* ---- pattern compiler (host only, no GPU needed) ------------------------ */
+/* Replaces regexp.Compile(pattern) inside regexp.Match (grep.go:21) with Go
+ * regexp/syntax Perl-flag semantics. A pattern Go rejects still returns
+ * DGREP_OK with a blob flagged DGREP_DFA_GO_SYNTAX_ERROR|MATCH_NONE, because
+ * the reference discards the error and matches nothing. `err` (optional)
+ * receives a message for non-OK results. */
+int dgrep_compile(const char* pattern, size_t n, void** blob, size_t* blob_len, char* err, size_t errlen);
+void dgrep_blob_free(void* blob);
+int dgrep_blob_info_get(const void* blob, size_t n, dgrep_blob_info* info);
+
+/* ---- device context ------------------------------------------------------ */
+int dgrep_open(int device, dgrep_ctx** ctx);
+void dgrep_close(dgrep_ctx* ctx);
+const char* dgrep_last_error(dgrep_ctx* ctx);
+/* Use an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL selects the context's own stream. */
+int dgrep_set_stream(dgrep_ctx* ctx, void* hip_stream);
+int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
+
+/* Host bytes -> H2D -> scan -> D2H results. This is the call Map makes. */
+int dgrep_scan(dgrep_ctx* ctx, const uint8_t* data, size_t n, dgrep_result* out);
+void dgrep_result_free(dgrep_result* r);
+
+/* HBM-resident split (the data never leaves the device): results are written
+ * to caller-provided device arrays of `capacity` entries; *count receives
+ * the number of matching lines (if > capacity, nothing beyond capacity is
+ * written: call again with a larger capacity). Asynchronous on the context
+ * stream except for the 8-byte count readback. */
+int dgrep_scan_device(dgrep_ctx* ctx, const void* d_data, size_t n, uint64_t* d_line_no, uint64_t* d_start,
+                      uint32_t* d_len, uint64_t capacity, uint64_t* count);
+
+/* ---- bench / test tooling ------------------------------------------------ */
+/* Fill d_out[0:n) with the seeded synthetic log corpus on
+ * the device. kind: 0 = plain log lines, 1 = log lines with seeded
+ * case-insensitive keywords planted (config 4). */
+int dgrep_synth_corpus(dgrep_ctx* ctx, void* d_out, size_t n, uint64_t seed, int kind);
+/* Host twin of dgrep_synth_corpus (same generator code): fills out[0:n). */
+int dgrep_synth_corpus_host(void* out, size_t n, uint64_t seed, int kind);
+/* Keyword i (0..999) of the seeded config-4 keyword set; returns its length. */
+int dgrep_synth_keyword(uint64_t seed, int i, char* out16);
+/* Average device time (ms) of the scan kernel over the last dgrep_scan*
+ * call, measured with HIP events on the launch stream. */
+int dgrep_last_kernel_ms(dgrep_ctx* ctx, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

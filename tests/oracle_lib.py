@@ -1,0 +1,121 @@
+"""ctypes binding of the ORACLE (oracle/liboracle.so) — test infrastructure only.
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+checker; the product path (libdgrep.so) never loads it.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+ORC_OK, ORC_ESYNTAX, ORC_EUNSUPPORTED = 0, 1, 2
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle not built: run `make -C oracle` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_compile.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                                  ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_compile.restype = ctypes.c_int
+        L.orc_match.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_match.restype = ctypes.c_int
+        L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_free.restype = None
+        for fn in (L.orc_map,):
+            fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+            fn.restype = ctypes.c_int64
+        L.orc_map_mt.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_map_mt.restype = ctypes.c_int64
+        L.orc_ihash.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_ihash.restype = ctypes.c_uint32
+        L.orc_format_key.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_char_p,
+                                     ctypes.c_size_t]
+        L.orc_format_key.restype = ctypes.c_size_t
+        L.orc_json_kv.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                  ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_json_kv.restype = ctypes.c_size_t
+        _lib = L
+    return _lib
+
+
+class Regexp:
+    """Go regexp.Compile(pattern) restated; .match(line) = regexp.Match."""
+
+    def __init__(self, pattern: bytes):
+        if isinstance(pattern, str):
+            pattern = pattern.encode()
+        self.pattern = pattern
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(256)
+        self.status = lib().orc_compile(pattern, len(pattern), ctypes.byref(h), err, 256)
+        self.error = err.value.decode(errors="replace")
+        self._h = h
+
+    def match(self, line: bytes) -> bool:
+        if isinstance(line, str):
+            line = line.encode()
+        return bool(lib().orc_match(self._h, line, len(line)))
+
+    def __del__(self):
+        try:
+            lib().orc_free(self._h)
+        except Exception:
+            pass
+
+
+def compile_status(pattern: bytes) -> int:
+    return Regexp(pattern).status
+
+
+def grep_map(pattern: bytes, contents: bytes, recompile_per_line=False, threads=0):
+    """grep.go Map restated: returns (line_no u64[], start u64[], len u32[])."""
+    if isinstance(pattern, str):
+        pattern = pattern.encode()
+    buf = np.frombuffer(contents, dtype=np.uint8) if len(contents) else np.zeros(1, np.uint8)
+    ptr = buf.ctypes.data
+    L = lib()
+    cap = 0
+    for _ in range(2):
+        ln = np.zeros(max(cap, 1), np.uint64)
+        st = np.zeros(max(cap, 1), np.uint64)
+        lens = np.zeros(max(cap, 1), np.uint32)
+        if threads and threads > 1:
+            cnt = L.orc_map_mt(pattern, len(pattern), ptr, len(contents), threads, ln.ctypes.data,
+                               st.ctypes.data, lens.ctypes.data, cap)
+        else:
+            cnt = L.orc_map(pattern, len(pattern), ptr, len(contents), int(recompile_per_line), ln.ctypes.data,
+                            st.ctypes.data, lens.ctypes.data, cap)
+        if cnt < 0:
+            raise NotImplementedError("pattern unsupported by the oracle: %r" % pattern)
+        if cnt <= cap:
+            return ln[:cnt], st[:cnt], lens[:cnt]
+        cap = cnt
+    raise AssertionError("unreachable")
+
+
+def ihash(key: bytes) -> int:
+    return lib().orc_ihash(key, len(key))
+
+
+def format_key(filename: bytes, line: int) -> bytes:
+    n = lib().orc_format_key(filename, len(filename), line, None, 0)
+    out = ctypes.create_string_buffer(n)
+    lib().orc_format_key(filename, len(filename), line, out, n)
+    return out.raw[:n]
+
+
+def json_kv(key: bytes, value: bytes) -> bytes:
+    n = lib().orc_json_kv(key, len(key), value, len(value), None, 0)
+    out = ctypes.create_string_buffer(n)
+    lib().orc_json_kv(key, len(key), value, len(value), out, n)
+    return out.raw[:n]

@@ -1,0 +1,169 @@
+"""GPU parity: libdgrep.so (HIP, gfx950) against the CPU oracle.
+
+Every test calls the product through its C ABI (dgrep_scan / dgrep_scan_device)
+and compares bit-exactly with the oracle's restatement of grep.go Map
+(oracle/, parity unpinned — see oracle/oracle.h). Sizes are chosen so the
+oracle finishes in seconds; full-size runs are covered by bench.py's
+size-independent checks.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+PATTERNS = [
+    b"error",
+    b"",
+    b"^$",
+    b"(?i)ERROR",
+    b"timeout while waiting for lock",
+    b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+",
+    b"\\bkey\\b",
+    b"k$",
+    b"^2024-0[1-3]",
+    b"[^a-z ]{3}",
+    b"\\x{FFFD}",
+    b"^[ -~]{45}$",
+    b"(?i)k",
+    b"a**",  # Go syntax error: nothing matches
+    b"e(r|x)+o",
+]
+
+
+def _oracle(pattern, data, threads=1):
+    ln, st, le = O.grep_map(pattern, data, threads=threads)
+    return ln, st, le
+
+
+def _check(ctx, pattern, data, threads=1):
+    ctx.load(pattern)
+    ln, st, le = ctx.scan(data)
+    oln, ost, ole = _oracle(pattern, data, threads)
+    assert len(ln) == len(oln), (pattern, len(ln), len(oln))
+    np.testing.assert_array_equal(ln, oln)
+    np.testing.assert_array_equal(st, ost)
+    np.testing.assert_array_equal(le, ole)
+    return len(ln)
+
+
+def test_synth_device_matches_host(gpu_ctx):
+    import torch
+    import dgrep
+
+    n = (1 << 20) + 12345
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu_ctx.synth(buf.data_ptr(), n, 7, 1)
+    torch.cuda.synchronize()
+    host = dgrep.synth_corpus_host(n, 7, 1)
+    assert buf.cpu().numpy().tobytes() == host
+
+
+@pytest.mark.parametrize("pattern", PATTERNS)
+def test_edge_inputs(gpu_ctx, pattern):
+    cases = [b"", b"\n", b"\n\n", b"error", b"error\n", b"x\nerror", b"\nerror\n\n", b"key\nk\n",
+             b"\xff\xfe\n\xe2\x82\xac\n\xe2\x82\n", b"a" * 5000 + b"error" + b"b" * 5000 + b"\nerror"]
+    for data in cases:
+        _check(gpu_ctx, pattern, data)
+
+
+@pytest.mark.parametrize("pattern", PATTERNS)
+def test_random_small(gpu_ctx, pattern):
+    rnd = random.Random(hash(pattern) & 0xffff)
+    alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b"K", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\r", b"\xe2\x82\xac",
+             b"\xe2\x82", b"\xff", b"\xc5\xbf", b"WARN", b"ERROR", b"error", b"2024-01", b"key "]
+    for _ in range(20):
+        n = rnd.choice([10, 100, 1000, 70000, 300000])
+        data = b"".join(rnd.choice(alpha) for _ in range(n // 3))
+        _check(gpu_ctx, pattern, data)
+
+
+@pytest.mark.parametrize("size", [1, 63, 64, 1023, 1024, 1025, 262143, 262144, 262145, 3 * 262144 + 17])
+def test_tile_and_chunk_boundaries(gpu_ctx, size):
+    import dgrep
+
+    data = bytearray(dgrep.synth_corpus_host(size, 11, 0))
+    # force lines that end / start exactly at chunk and tile edges
+    for edge in (1023, 1024, 2047, 262143, 262144):
+        if edge < size:
+            data[edge] = 0x0A
+    data = bytes(data)
+    for pattern in (b"error", b"", b"^2024", b"ok$"):
+        _check(gpu_ctx, pattern, data)
+
+
+def test_long_lines_cross_many_chunks(gpu_ctx):
+    rnd = random.Random(3)
+    parts = []
+    for i in range(40):
+        L = rnd.choice([10, 5000, 300000, 70000])
+        body = bytes(rnd.choice(b"abcdefghij ") for _ in range(L))
+        if rnd.random() < 0.5:
+            p = rnd.randrange(L)
+            body = body[:p] + b"error" + body[p:]
+        parts.append(body)
+    data = b"\n".join(parts)
+    for pattern in (b"error", b"^[a-j ]*$", b"error$", b""):
+        _check(gpu_ctx, pattern, data)
+
+
+def test_dense_matches_overflow_slots(gpu_ctx):
+    # every line matches and lines are short: lanes own far more matching lines
+    # than their LDS slots and take the direct-write path
+    data = b"\n".join(b"error %d" % i for i in range(200000))
+    _check(gpu_ctx, b"error", data)
+    _check(gpu_ctx, b"", data)
+    data2 = b"\n" * 100000
+    _check(gpu_ctx, b"", data2)
+    _check(gpu_ctx, b"^$", data2)
+
+
+@pytest.mark.parametrize("seed,pattern", [(1, b"error"), (2, b"timeout while waiting for lock"),
+                                          (3, b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+")])
+def test_synth_corpus_vs_oracle(gpu_ctx, seed, pattern):
+    import dgrep
+
+    data = dgrep.synth_corpus_host(24 << 20, seed, 0)
+    n = _check(gpu_ctx, pattern, data, threads=16)
+    assert n > 0
+
+
+def test_scan_device_resident(gpu_ctx):
+    import torch
+    import dgrep
+
+    n = 32 << 20
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu_ctx.synth(buf.data_ptr(), n, 1, 0)
+    gpu_ctx.load(b"error")
+    cap = 1 << 20
+    ln = torch.empty(cap, dtype=torch.int64, device="cuda")
+    st = torch.empty(cap, dtype=torch.int64, device="cuda")
+    le = torch.empty(cap, dtype=torch.int32, device="cuda")
+    cnt = gpu_ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), cap)
+    host = buf.cpu().numpy().tobytes()
+    oln, ost, ole = O.grep_map(b"error", host, threads=16)
+    assert cnt == len(oln)
+    np.testing.assert_array_equal(ln[:cnt].cpu().numpy().astype(np.uint64), oln)
+    np.testing.assert_array_equal(st[:cnt].cpu().numpy().astype(np.uint64), ost)
+    np.testing.assert_array_equal(le[:cnt].cpu().numpy().astype(np.uint32), ole)
+    # capacity too small: count reported, caller retries
+    cnt2 = gpu_ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), 10)
+    assert cnt2 == cnt
+
+
+def test_map_reduce_surface(gpu_ctx):
+    import dgrep
+
+    dgrep.set_pattern("error")
+    kva = dgrep.Map("log.txt", "ok\nan error\nerror\n")
+    assert kva == [dgrep.KeyValue("log.txt (line number #2)", "an error"),
+                   dgrep.KeyValue("log.txt (line number #3)", "error")]
+    assert dgrep.Reduce(kva[0].Key, [kva[0].Value, "x"]) == "an error"
+    dgrep.set_pattern("")
+    assert len(dgrep.Map("f", "a\nb\n")) == 3  # trailing empty line matches ""
+    dgrep.set_pattern("a**")
+    assert dgrep.Map("f", "a\n") == []
