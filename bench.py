@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""bench.py — the distributed-grep Map hot path on MI355X.
+
+One *step* = one pass of the Map hot path (application/grep.go:17-29: split on
+'\\n' + regexp.Match per line) over one HBM-resident synthetic split, producing
+the matching lines' (line_no, start, len) records in HBM (dgrep_scan_device).
+With N > 1 ranks (one process per GPU, torch.distributed over RCCL), every rank
+scans its own split (Map tasks shard per split, map_reduce/coordinator.go:312)
+and the compacted match records are gathered to rank 0 over xGMI in the same
+step — the only exchange the path has.
+
+Default workload (N=1): BASELINE.json configs[1] = SURVEY §8d C2: a 16 GiB
+seeded synthetic log split, literal pattern `error`, LDS-resident DFA.
+`value` = whole-job GB/s of text scanned (sum over ranks / max-over-ranks
+time); `roofline` = the scan kernel's algorithmic bytes (split bytes read +
+16 B per staged match) / its HIP-event time against the 8 TB/s HBM peak;
+`cpu_baseline` = the oracle's restatement of grep.go Map (per-line
+regexp compile, as grep.go:21 does) on one host core, on a bounded prefix
+sample of the same split.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+STAGED_LINE_BYTES = 16  # StagedLine written by the scan kernel per match
+
+WORKLOADS = {
+    "c2": dict(pattern="error", seed=2, kind=0, gib=16.0,
+               desc="C2: 16 GiB synthetic log split (seed 2), literal 'error', LDS-resident DFA"),
+    "c2b": dict(pattern="timeout while waiting for lock", seed=2, kind=0, gib=16.0,
+                desc="C2 (long planted literal): 16 GiB split (seed 2)"),
+    "c3": dict(pattern="^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", seed=3, kind=0, gib=16.0,
+               desc="C3: 16 GiB split (seed 3), anchored regex with classes/alternation"),
+}
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--split-gib", type=float, default=None, help="per-GPU split size (default: workload's)")
+    ap.add_argument("--cpu-sample-mib", type=int, default=96)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify-windows", type=int, default=6)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import dgrep
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    wl = WORKLOADS[args.workload]
+    gib = args.split_gib if args.split_gib is not None else wl["gib"]
+    n = int(gib * (1 << 30))
+    n -= n % 64
+    pattern = wl["pattern"]
+
+    ctx = dgrep.Context(local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    cp = ctx.load(pattern)
+
+    t = time.time()
+    buf = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+    ctx.synth(buf.data_ptr(), n, wl["seed"] + 1000 * rank, wl["kind"])
+    torch.cuda.synchronize(dev)
+    log("rank %d: generated %.1f GiB split in %.1fs; DFA %d states x %d classes" %
+        (rank, n / 2**30, time.time() - t, cp.nstates, cp.nclasses))
+
+    # size the result arrays from a first scan (capacity-retry protocol of the ABI)
+    cap = max(1 << 16, n // 4096)
+    res = None
+    for _ in range(3):
+        res = (torch.empty(cap, dtype=torch.int64, device=dev), torch.empty(cap, dtype=torch.int64, device=dev),
+               torch.empty(cap, dtype=torch.int32, device=dev))
+        cnt = ctx.scan_device(buf.data_ptr(), n, res[0].data_ptr(), res[1].data_ptr(), res[2].data_ptr(), cap)
+        if cnt <= cap:
+            break
+        cap = int(cnt * 1.05) + 1024
+    line_t, start_t, len_t = res
+
+    gather_buf = None
+
+    def step():
+        c = ctx.scan_device(buf.data_ptr(), n, line_t.data_ptr(), start_t.data_ptr(), len_t.data_ptr(), cap)
+        if world > 1:
+            nonlocal gather_buf
+            cnt_t = torch.tensor([c], dtype=torch.int64, device=dev)
+            counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+            dist.all_gather(counts, cnt_t)
+            mx = int(torch.stack(counts).max().item())
+            rec = torch.zeros((3, max(mx, 1)), dtype=torch.int64, device=dev)
+            rec[0, :c] = line_t[:c]
+            rec[1, :c] = start_t[:c]
+            rec[2, :c] = len_t[:c].to(torch.int64)
+            if rank == 0:
+                gather_buf = [torch.empty_like(rec) for _ in range(world)]
+                dist.gather(rec, gather_list=gather_buf, dst=0)
+            else:
+                dist.gather(rec, dst=0)
+        return c
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kms = []
+    t0 = time.perf_counter()
+    count = 0
+    for _ in range(args.steps):
+        count = step()
+        kms.append(ctx.last_kernel_ms())
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms_step = elapsed / args.steps * 1e3
+    value = world * n * args.steps / elapsed / 1e9
+    kern_ms = float(np.mean(kms))
+    achieved = (n + STAGED_LINE_BYTES * count) / (kern_ms * 1e-3) / 1e9
+
+    # ---- size-independent checks on the full split (rank 0) ----------------
+    verified = None
+    if rank == 0 and args.verify_windows > 0:
+        verified = verify_windows(buf, n, line_t[:count], start_t[:count], len_t[:count], pattern,
+                                  args.verify_windows)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(buf, n, pattern, args.cpu_sample_mib)
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        try:
+            with open(tpath) as f:
+                tr = json.load(f).get(args.workload)
+            if tr and abs(tr.get("split_bytes", 0) - n) < 1024:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "GB/s text scanned per GPU and whole node (1/2/4/8×MI355X), % of HBM peak",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded log corpus generated in HBM, SURVEY.md §8d)",
+            "config": {
+                "workload": wl["desc"] if world == 1 else wl["desc"] + "; one split per GPU + RCCL gather of match records to rank 0",
+                "pattern": pattern,
+                "split_bytes_per_gpu": n,
+                "total_bytes": n * world,
+                "matching_lines_per_split": int(count),
+                "dfa_states": cp.nstates,
+                "dfa_byte_classes": cp.nclasses,
+                "parallelism": "1 split per GPU x %d" % world,
+                "per_gpu_gbs": round(value / world, 2),
+                "hbm_frac_whole_node": round(value / (HBM_PEAK_GBS * world), 4),
+                "verified_windows": verified,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "dgrep::scan_dfa8_kernel",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms_avg": round(kern_ms, 4),
+                "algorithmic_bytes_per_launch": int(n + STAGED_LINE_BYTES * count),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def verify_windows(buf, n, line_t, start_t, len_t, pattern, k):
+    """Parity at full size: random whole-line windows of the split re-run on the
+    oracle (lines renumbered by the '\\n' count before the window, counted on the
+    GPU) must equal the GPU records inside the window; records must be strictly
+    ascending."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    if line_t.numel() > 1:
+        assert bool((line_t[1:] > line_t[:-1]).all()), "line numbers not strictly ascending"
+    rng = np.random.default_rng(12345)
+    win = 2 << 20
+    ok = 0
+    for _ in range(k):
+        a0 = int(rng.integers(0, max(1, n - win)))
+        chunk = buf[a0:min(n, a0 + win)].cpu().numpy().tobytes()
+        i = chunk.find(b"\n")
+        j = chunk.rfind(b"\n")
+        if i < 0 or j <= i:
+            continue
+        a, b = a0 + i + 1, a0 + j  # whole lines [a, b), b = a '\n'
+        text = chunk[i + 1:j]
+        nl_before = int((buf[:a] == 10).sum().item())
+        oln, ost, ole = O.grep_map(pattern.encode(), text)
+        sel = (start_t >= a) & (start_t < b)
+        gl = line_t[sel].cpu().numpy().astype(np.int64)
+        gs = start_t[sel].cpu().numpy().astype(np.int64)
+        ge = len_t[sel].cpu().numpy().astype(np.int64)
+        np.testing.assert_array_equal(gl, oln.astype(np.int64) + nl_before)
+        np.testing.assert_array_equal(gs, ost.astype(np.int64) + a)
+        np.testing.assert_array_equal(ge, ole.astype(np.int64))
+        ok += 1
+    return ok
+
+
+def cpu_baseline(buf, n, pattern, sample_mib):
+    """The oracle's restatement of grep.go Map on one host core: per line,
+    regexp.Match(pattern, line) recompiles the pattern (grep.go:21) — the
+    reference's own algorithm, not a tuned CPU grep."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    m = min(n, sample_mib << 20)
+    data = buf[:m].cpu().numpy().tobytes()
+    j = data.rfind(b"\n")
+    data = data[: j + 1] if j >= 0 else data
+    t = time.perf_counter()
+    ln, _, _ = O.grep_map(pattern.encode(), data, recompile_per_line=True)
+    dt = time.perf_counter() - t
+    return {
+        "value": round(len(data) / dt / 1e9, 5),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "first %.0f MiB of the same split (%d matching lines), oracle/ grep.go Map restatement with "
+                  "per-line pattern compile, 1 thread, %.1f s" % (len(data) / 2**20, len(ln), dt),
+    }
+
+
+if __name__ == "__main__":
+    main()
