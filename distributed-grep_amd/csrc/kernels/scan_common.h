@@ -21,6 +21,15 @@ struct TileInfo {
   uint32_t nl;     // '\n' bytes inside the tile
 };
 
+// A lane whose matching lines overflowed its LDS slots (re-run by
+// scan_overflow_kernel in direct-write mode).
+struct OverflowLane {
+  uint64_t cs;         // chunk start
+  uint64_t out_base;   // its first staging index
+  uint32_t nl_prefix;  // '\n' between the tile start and cs
+  uint32_t pad;
+};
+
 struct ScanArgs {
   const uint8_t* data;
   uint64_t n;
@@ -34,6 +43,9 @@ struct ScanArgs {
   unsigned long long* counter;  // staging append counter
   TileInfo* tiles;
   uint32_t* status;       // error bits (kStatus*)
+  OverflowLane* overflow;
+  uint64_t overflow_cap;
+  unsigned long long* overflow_count;
 };
 
 enum : uint32_t { kStatusLineTooLong = 1u };

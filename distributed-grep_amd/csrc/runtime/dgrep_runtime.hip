@@ -21,9 +21,10 @@
 namespace dgrep {
 // scan_dfa.hip
 uint64_t scan_tile_bytes();
-size_t scan_dfa8_lds_bytes(uint32_t table_bytes);
+uint32_t scan_table_row();
 hipError_t scan_dfa8_occupancy(uint32_t table_bytes, int* blocks_per_cu);
 hipError_t scan_dfa8(const ScanArgs& a, int grid, hipStream_t stream);
+hipError_t scan_dfa8_overflow(const ScanArgs& a, uint64_t nover, hipStream_t stream);
 hipError_t tile_scan(TileInfo* tiles, uint64_t ntiles, uint64_t* out_off, uint64_t* line_base, hipStream_t stream);
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, const uint64_t* out_off,
                        const uint64_t* line_base, uint64_t capacity, uint64_t* line_no, uint64_t* start,
@@ -43,7 +44,7 @@ struct dgrep_ctx {
   bool loaded = false;
   uint32_t flags = 0, nstates = 0, start = 0, start_m = 0;
   bool empty_line_matches = false;
-  uint8_t* d_table = nullptr;  // u8 [state][byte]
+  uint8_t* d_table = nullptr;  // u8 [state][byte], row stride scan_table_row()
   uint32_t table_bytes = 0;
   int blocks_per_cu = 1;
 
@@ -54,8 +55,10 @@ struct dgrep_ctx {
   uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0;
   StagedLine* d_staging = nullptr;
   uint64_t staging_cap = 0;
-  unsigned long long* d_counter = nullptr;
-  uint32_t* d_status = nullptr;
+  // device counters: [0] staging append counter, [1] overflow lanes, [2] status bits
+  unsigned long long* d_counters = nullptr;
+  OverflowLane* d_overflow = nullptr;
+  uint64_t overflow_cap = 0;
 
   // dgrep_scan (host data) buffers
   uint8_t* d_data = nullptr;
@@ -104,8 +107,7 @@ extern "C" int dgrep_open(int device, dgrep_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_counter), sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_status), sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), 4 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     // keep the context so the caller can read the message
     c->err = std::string("dgrep_open: ") + hipGetErrorString(e);
@@ -121,8 +123,8 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counter,
-                  c->d_status, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len};
+  void* bufs[] = {c->d_table, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
+                  c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -160,10 +162,12 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
              " states; this build scans DFAs of at most 256 states (LDS-resident u8 table)";
     return DGREP_E_UNSUPPORTED;
   }
-  // expand byte classes: table[s*256 + b] = trans[s][class(b)]
-  std::vector<uint8_t> t(size_t(h.nstates) * 256);
+  // expand byte classes into the kernel's LDS image: row s (stride
+  // scan_table_row() = 260, bank-staggered) holds trans[s][class(b)] at byte b
+  const size_t row = scan_table_row();
+  std::vector<uint8_t> t((size_t(h.nstates) * row + 15) & ~size_t(15), 0);
   for (uint32_t s = 0; s < h.nstates; ++s)
-    for (int b = 0; b < 256; ++b) t[size_t(s) * 256 + size_t(b)] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
+    for (int b = 0; b < 256; ++b) t[size_t(s) * row + size_t(b)] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
   if (c->d_table) HIPCHK(hipFree(c->d_table));
   c->d_table = nullptr;
   c->table_bytes = uint32_t(t.size());
@@ -213,6 +217,8 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   if ((rc = grow(c, &c->d_line_base, &c->lb_cap, ntiles + 1)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_staging, &c->staging_cap, capacity)) != DGREP_OK) return rc;
 
+  if (!c->d_overflow && (rc = grow(c, &c->d_overflow, &c->overflow_cap, 1u << 16)) != DGREP_OK) return rc;
+
   ScanArgs a;
   memset(&a, 0, sizeof a);
   a.data = d_data;
@@ -224,26 +230,33 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.ntiles = ntiles;
   a.staging = c->d_staging;
   a.capacity = capacity;
-  a.counter = c->d_counter;
+  a.counter = c->d_counters;
   a.tiles = c->d_tiles;
-  a.status = c->d_status;
-  HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_status, 0, 4, c->stream));
+  a.status = reinterpret_cast<uint32_t*>(c->d_counters + 2);
+  a.overflow_count = c->d_counters + 1;
   const uint64_t resident = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
   const int grid = int(std::min<uint64_t>(ntiles, resident));
-  HIPCHK(hipEventRecord(c->ev0, c->stream));
-  HIPCHK(scan_dfa8(a, grid, c->stream));
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
-  unsigned long long total = 0;
-  uint32_t status = 0;
-  HIPCHK(hipMemcpyAsync(&total, c->d_counter, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(&status, c->d_status, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  unsigned long long ctr[4] = {0, 0, 0, 0};
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    a.overflow = c->d_overflow;
+    a.overflow_cap = c->overflow_cap;
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    HIPCHK(scan_dfa8(a, grid, c->stream));
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    HIPCHK(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (ctr[1] <= c->overflow_cap) break;
+    // more overflowing lanes than recorded: grow the list and scan again
+    if ((rc = grow(c, &c->d_overflow, &c->overflow_cap, ctr[1])) != DGREP_OK) return rc;
+  }
   HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-  if (status & kStatusLineTooLong) {
+  const uint64_t total = ctr[0];
+  if (uint32_t(ctr[2]) & kStatusLineTooLong) {
     c->err = "a matching line is longer than 4 GiB (uint32 length in dgrep_result)";
     return DGREP_E_UNSUPPORTED;
   }
+  if (ctr[1] && total <= capacity) HIPCHK(scan_dfa8_overflow(a, ctr[1], c->stream));
   *count = total;
   if (total == 0 || total > capacity) return DGREP_OK;
   HIPCHK(tile_scan(c->d_tiles, ntiles, c->d_out_off, c->d_line_base, c->stream));

@@ -1,0 +1,248 @@
+// microbench_scan.hip — ablation micro-benchmark for the scan kernel's lane
+// loop (not part of the product). Each variant streams the same HBM-resident
+// text with the product's chunk-per-lane access pattern and adds one cost at a
+// time, so the profile of scan_dfa8_kernel can be attributed:
+//   V0c  coalesced 16 B/lane streaming read (bandwidth reference)
+//   V0   per-lane chunk streaming, 64-B blocks, prefetch 1 block
+//   V0b  per-lane chunk streaming, prefetch 2 blocks
+//   V1   V0 + DFA step per byte (LDS u8 table, 260-B rows)
+//   V2   V1 + SWAR newline count per word
+//   V3   V2 + per-word START_M check with a (never taken) branch
+//   V4   V2 with NS independent chunk streams interleaved per lane (ILP)
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/microbench_scan.hip -o tools/microbench_scan
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHK(x)                                                                      \
+  do {                                                                              \
+    hipError_t e = (x);                                                             \
+    if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } \
+  } while (0)
+
+constexpr int kT = 256;
+constexpr uint32_t kRow = 260;
+
+__device__ __forceinline__ uint32_t nl_mask(uint32_t w) {
+  uint32_t x = w ^ 0x0a0a0a0au;
+  uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
+  return ~t & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t step(const uint8_t* tbl, uint32_t s, uint32_t w, uint32_t sel) {
+  return tbl[__builtin_amdgcn_perm(s, w, sel) + (s << 2)];
+}
+
+struct Smem {
+  uint8_t tbl[16 * kRow];
+};
+
+template <int MODE>
+__device__ __forceinline__ void word(const uint8_t* tbl, uint32_t x, uint32_t& s, uint32_t& acc, uint32_t M,
+                                     uint32_t* flag) {
+  if (MODE == 0) {
+    acc ^= x;
+    return;
+  }
+  const uint32_t s0 = step(tbl, s, x, 0x0c0c0400u);
+  const uint32_t s1 = step(tbl, s0, x, 0x0c0c0401u);
+  const uint32_t s2 = step(tbl, s1, x, 0x0c0c0402u);
+  const uint32_t s3 = step(tbl, s2, x, 0x0c0c0403u);
+  if (MODE >= 2) acc += __popc(nl_mask(x));
+  if (MODE >= 3) {
+    if (__builtin_expect((s0 == M) | (s1 == M) | (s2 == M) | (s3 == M), 0)) atomicAdd(flag, 1u);
+  }
+  s = s3;
+}
+
+template <int MODE, int PF>
+__global__ __launch_bounds__(kT) void lane_kernel(const uint8_t* __restrict__ data, uint64_t n, int C,
+                                                  const uint8_t* table, uint32_t* out, uint32_t M) {
+  __shared__ Smem sm;
+  for (int i = threadIdx.x; i < int(sizeof(sm.tbl)); i += kT) sm.tbl[i] = table[i];
+  __syncthreads();
+  const uint64_t ntiles = n / (uint64_t(kT) * C);
+  uint32_t acc = 0, s = 0;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint4* p = reinterpret_cast<const uint4*>(data + t * uint64_t(kT) * C + uint64_t(threadIdx.x) * C);
+    const int nb = C / 64;
+    uint4 A[4], B[4], D[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A[i] = p[i];
+    if (PF == 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) B[i] = p[4 + i];
+    }
+    for (int b = 0; b < nb; ++b) {
+      if (PF == 1) {
+        const int nx = b + 1 < nb ? b + 1 : b;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) B[i] = p[nx * 4 + i];
+      } else {
+        const int nx = b + 2 < nb ? b + 2 : b;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) D[i] = p[nx * 4 + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        word<MODE>(sm.tbl, A[i].x, s, acc, M, out + 1);
+        word<MODE>(sm.tbl, A[i].y, s, acc, M, out + 1);
+        word<MODE>(sm.tbl, A[i].z, s, acc, M, out + 1);
+        word<MODE>(sm.tbl, A[i].w, s, acc, M, out + 1);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        A[i] = B[i];
+        if (PF == 2) B[i] = D[i];
+      }
+    }
+  }
+  if (acc == 0x12345678u && s == 77) out[0] = acc;  // keep live
+}
+
+// NS independent streams per lane: lane handles chunks tid and tid + kT*k
+template <int NS>
+__global__ __launch_bounds__(kT) void multi_kernel(const uint8_t* __restrict__ data, uint64_t n, int C,
+                                                   const uint8_t* table, uint32_t* out, uint32_t M) {
+  __shared__ Smem sm;
+  for (int i = threadIdx.x; i < int(sizeof(sm.tbl)); i += kT) sm.tbl[i] = table[i];
+  __syncthreads();
+  const uint64_t tile = uint64_t(kT) * C * NS;
+  const uint64_t ntiles = n / tile;
+  uint32_t acc = 0;
+  uint32_t s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) s[k] = 0;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint4* p[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      p[k] = reinterpret_cast<const uint4*>(data + t * tile + (uint64_t(k) * kT + threadIdx.x) * C);
+    const int nb = C / 64;
+    uint4 A[NS][4], B[NS][4];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) A[k][i] = p[k][i];
+    for (int b = 0; b < nb; ++b) {
+      const int nx = b + 1 < nb ? b + 1 : b;
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) B[k][i] = p[k][nx * 4 + i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t* wa[NS];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int k = 0; k < NS; ++k) {
+            const uint32_t x = q == 0 ? A[k][i].x : q == 1 ? A[k][i].y : q == 2 ? A[k][i].z : A[k][i].w;
+            word<2>(sm.tbl, x, s[k], acc, M, out + 1);
+          }
+        }
+        (void)wa;
+      }
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A[k][i] = B[k][i];
+    }
+  }
+  uint32_t z = acc;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) z ^= s[k];
+  if (z == 0x12345678u) out[0] = z;
+}
+
+__global__ void coalesced_kernel(const uint4* __restrict__ d, uint64_t n16, uint32_t* out) {
+  uint32_t acc = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x) {
+    uint4 v = d[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+__global__ void fill_kernel(uint8_t* d, uint64_t n) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    uint64_t h = i * 0x9e3779b97f4a7c15ull;
+    h ^= h >> 29;
+    uint8_t c = uint8_t('a' + (h % 26));
+    if ((h >> 8) % 120 == 0) c = '\n';
+    if ((h >> 16) % 9 == 0) c = ' ';
+    d[i] = c;
+  }
+}
+
+template <class F>
+float timeit(F f, int reps) {
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  f();
+  CHK(hipDeviceSynchronize());
+  CHK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) f();
+  CHK(hipEventRecord(b));
+  CHK(hipEventSynchronize(b));
+  float ms;
+  CHK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+int main(int argc, char** argv) {
+  const uint64_t n = uint64_t(argc > 1 ? atoi(argv[1]) : 4) << 30;
+  const int C = argc > 2 ? atoi(argv[2]) : 1024;
+  int cus = 0;
+  CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  uint8_t* d;
+  uint32_t* out;
+  uint8_t* tbl;
+  CHK(hipMalloc(&d, n + 4096));
+  CHK(hipMalloc(&out, 64));
+  CHK(hipMalloc(&tbl, 16 * kRow));
+  fill_kernel<<<4096, 256>>>(d, n);
+  // 'error' DFA-like table: 7 states, mostly back to 0
+  std::vector<uint8_t> h(16 * kRow, 0);
+  const char* pat = "error";
+  for (int s = 0; s < 6; ++s)
+    for (int b = 0; b < 256; ++b) {
+      int nx = (b == pat[0]) ? 1 : 0;
+      if (s < 5 && b == pat[s]) nx = s + 1;
+      if (s == 5) nx = 5;
+      if (b == '\n') nx = (s == 5) ? 6 : 0;
+      h[s * kRow + b] = uint8_t(nx);
+    }
+  for (int b = 0; b < 256; ++b) h[6 * kRow + b] = h[0 * kRow + b];
+  CHK(hipMemcpy(tbl, h.data(), h.size(), hipMemcpyHostToDevice));
+  CHK(hipDeviceSynchronize());
+  const uint32_t M = 6;
+  auto gbs = [&](float ms) { return double(n) / (ms * 1e-3) / 1e9; };
+  const int reps = 5;
+  for (int occ : {4, 5, 6, 8}) {
+    const int grid = cus * occ;
+    printf("--- grid %d WGs (%d per CU), C=%d, n=%.1f GiB\n", grid, occ, C, n / double(1 << 30));
+    float ms;
+    ms = timeit([&] { coalesced_kernel<<<grid, kT>>>(reinterpret_cast<const uint4*>(d), n / 16, out); }, reps);
+    printf("V0c coalesced        %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { lane_kernel<0, 1><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V0  lane stream pf1  %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { lane_kernel<0, 2><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V0b lane stream pf2  %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { lane_kernel<1, 1><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V1  + DFA            %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { lane_kernel<1, 2><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V1b + DFA pf2        %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { lane_kernel<2, 1><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V2  + newline SWAR   %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { lane_kernel<3, 1><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V3  + event branch   %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { multi_kernel<2><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V4  V2 x2 streams    %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { multi_kernel<4><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
+    printf("V4  V2 x4 streams    %8.1f GB/s\n", gbs(ms));
+  }
+  return 0;
+}
