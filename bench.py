@@ -103,25 +103,13 @@ def main():
         cap = int(cnt * 1.05) + 1024
     line_t, start_t, len_t = res
 
-    gather_buf = None
+    from dgrep.dist import gather_records
 
     def step():
         c = ctx.scan_device(buf.data_ptr(), n, line_t.data_ptr(), start_t.data_ptr(), len_t.data_ptr(), cap)
         if world > 1:
-            nonlocal gather_buf
-            cnt_t = torch.tensor([c], dtype=torch.int64, device=dev)
-            counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-            dist.all_gather(counts, cnt_t)
-            mx = int(torch.stack(counts).max().item())
-            rec = torch.zeros((3, max(mx, 1)), dtype=torch.int64, device=dev)
-            rec[0, :c] = line_t[:c]
-            rec[1, :c] = start_t[:c]
-            rec[2, :c] = len_t[:c].to(torch.int64)
-            if rank == 0:
-                gather_buf = [torch.empty_like(rec) for _ in range(world)]
-                dist.gather(rec, gather_list=gather_buf, dst=0)
-            else:
-                dist.gather(rec, dst=0)
+            # the path's only exchange: compacted records -> rank 0 over RCCL/xGMI
+            gather_records(line_t, start_t, len_t, c, dst=0)
         return c
 
     for _ in range(args.warmup):

@@ -50,6 +50,13 @@ struct ScanArgs {
 
 enum : uint32_t { kStatusLineTooLong = 1u };
 
-constexpr int kScanThreads = 256;
+constexpr int kScanThreads = 256;  // 4 waves per workgroup
+constexpr int kTileLanes = 64;     // a tile is one wave's 64 chunks
+
+// DFA stepper selected by dgrep_load_dfa from the state count.
+enum : int {
+  kStepTable = 0,   // <= 256 states: u8 [state][byte] table, 260-byte rows
+  kStepSheng8 = 1,  // <= 8 states: per-byte 8-state vectors (v_perm stepping)
+};
 
 }  // namespace dgrep

@@ -10,7 +10,7 @@
 // pass over the split evaluates every line.
 //
 // Work decomposition (HBM-bound: every input byte is read once):
-//   * tile = 256 lanes x C bytes; lane i owns chunk i of its tile.
+//   * tile = one wave = 64 lanes x C bytes; lane i owns chunk i of its tile.
 //   * A lane OWNS the lines that start inside its chunk after its first '\n'
 //     (the very first line of the split is owned by global lane 0). It runs the
 //     DFA from its chunk start -- the bytes before its first '\n' are run with a
@@ -19,19 +19,45 @@
 //     owned line's terminator) or the end of the split. No lane ever waits for
 //     another lane's state; a line longer than a chunk is simply run to its end
 //     by the lane that owns it.
-//   * Per 4-byte word: 4 x (v_perm_b32 + ds_read_u8) DFA steps from an
-//     LDS-resident u8 table [state][byte]; newline bookkeeping by SWAR on the
-//     word; a matching line is detected by "state == START_M" (rare path).
+//   * Per 4-byte word: 4 DFA steps by one of two steppers (below), newline
+//     bookkeeping by SWAR on the word, and a matching line is detected by
+//     "state == START_M" (rare path).
+//       StepSheng8 (DFA <= 8 states): LDS holds, per input byte b, the 8-byte
+//         vector V[b][s] = next state; a step is ONE v_perm_b32 selecting byte
+//         s of V[b] (SDWA does the byte extract for the ds_read_b64 address).
+//         The dependent chain is a single VALU op per byte; the LDS reads do
+//         not depend on the state, so their latency overlaps.
+//       StepTable (DFA <= 256 states): u8 table [state][byte] with 260-byte
+//         rows (bank-staggered); a step is v_perm (row|byte) + v_lshl_add +
+//         ds_read_u8 on the dependent chain.
 //   * Matching lines are parked in per-lane LDS slots, counted, then the tile's
 //     lines are appended to a staging buffer with ONE atomic per tile, in
-//     ascending order inside the tile. A second pass (dgrep_order_lines)
-//     turns tile-relative line numbers into global ones and lays the tiles out
-//     in split order.
+//     ascending order inside the tile (no workgroup barrier anywhere: waves
+//     are independent). Three small passes (tile_reduce / block_scan /
+//     order_lines) turn tile-relative line numbers into global ones and lay
+//     the tiles out in split order.
 #include <hip/hip_runtime.h>
 
 #include "scan_common.h"
 
+// build-time tuning knobs (defaults are the shipped configuration)
+#ifndef DGREP_CHUNK
+#define DGREP_CHUNK 4096
+#endif
+#ifndef DGREP_SLOTS
+#define DGREP_SLOTS 24
+#endif
+#ifndef DGREP_BLOCK
+#define DGREP_BLOCK 128  // bytes per lane per load block (64 or 128)
+#endif
+#ifndef DGREP_SHENG_SCHED_BARRIER
+#define DGREP_SHENG_SCHED_BARRIER 0
+#endif
+
 namespace dgrep {
+
+constexpr int kBlk = DGREP_BLOCK;
+static_assert(kBlk == 64 || kBlk == 128, "DGREP_BLOCK must be 64 or 128");
 
 __device__ __forceinline__ uint32_t nl_mask(uint32_t w) {
   // exact per-byte zero test of w ^ '\n\n\n\n': bit 7 of byte k set iff byte k == '\n'
@@ -48,14 +74,68 @@ constexpr uint32_t kRow = 260;
 
 template <int TBL, int E>
 struct ScanSmem {
-  uint8_t tbl[TBL];  // first member: the table sits at LDS address 0
+  alignas(16) uint8_t tbl[TBL];  // first member: the table sits at LDS address 0
   uint32_t slots[kScanThreads * E * 2];
-  uint32_t scratch[16];
 };
 
-__device__ __forceinline__ uint32_t dfa_step(const uint8_t* tbl, uint32_t s, uint32_t w, uint32_t sel) {
-  // v_perm builds (s << 8) | byte(w); + 4s staggers the row: tbl[s*260 + byte]
-  return tbl[__builtin_amdgcn_perm(s, w, sel) + (s << 2)];
+// DFA of at most 256 states: u8 transition table, row s at LDS s*260.
+struct StepTable {
+  static constexpr int kKind = kStepTable;
+  const uint8_t* tbl;
+  __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t w, uint32_t sel) const {
+    // v_perm builds (s << 8) | byte(w); + 4s staggers the row: tbl[s*260 + byte]
+    return tbl[__builtin_amdgcn_perm(s, w, sel) + (s << 2)];
+  }
+  // the whole step depends on the state: nothing to issue ahead
+  struct Pre {
+    uint32_t x;
+  };
+  __device__ __forceinline__ Pre prep(uint32_t x) const { return Pre{x}; }
+  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                        uint32_t& s3) const {
+    s0 = one(s, p.x, 0x0c0c0400u);
+    s1 = one(s0, p.x, 0x0c0c0401u);
+    s2 = one(s1, p.x, 0x0c0c0402u);
+    s3 = one(s2, p.x, 0x0c0c0403u);
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return tbl[s * kRow + b]; }
+  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
+};
+
+// DFA of at most 8 states (Sheng-style): V[b] = 8 next-state bytes. Only byte
+// 0 of the carried state is meaningful; v_perm fills bytes 1-3 with other
+// (valid, < 8) states, which never reach byte 0 of a later result.
+struct StepSheng8 {
+  static constexpr int kKind = kStepSheng8;
+  const uint2* V;
+  __device__ __forceinline__ static uint32_t sel(const uint2 v, uint32_t s) {
+    return __builtin_amdgcn_perm(v.y, v.x, s);
+  }
+  // the four LDS reads depend only on the input word: issued a word ahead
+  struct Pre {
+    uint2 m0, m1, m2, m3;
+  };
+  __device__ __forceinline__ Pre prep(uint32_t x) const {
+    return Pre{V[x & 0xffu], V[(x >> 8) & 0xffu], V[(x >> 16) & 0xffu], V[x >> 24]};
+  }
+  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                        uint32_t& s3) const {
+    s0 = sel(p.m0, s);
+    s1 = sel(p.m1, s0);
+    s2 = sel(p.m2, s1);
+    s3 = sel(p.m3, s2);
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[b], s); }
+  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return (s & 0xffu) == M; }
+};
+
+template <class Step>
+__device__ __forceinline__ Step make_step(const uint8_t* lds);
+template <>
+__device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds) { return StepTable{lds}; }
+template <>
+__device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds) {
+  return StepSheng8{reinterpret_cast<const uint2*>(lds)};
 }
 
 // Per-lane run state. Positions are relative to the lane's chunk start `cs`.
@@ -107,24 +187,24 @@ struct Blk {
   int lastj;        // its index
 };
 
-template <int J, int E, bool DIRECT>
-__device__ __forceinline__ void word_step(const uint8_t* tbl, uint32_t M, uint32_t x, uint32_t& s, Blk& b,
-                                          LaneRun& r, const Emitter<E, DIRECT>& emit) {
-  // keep each word's work in place: hoisting the (chain-independent) newline
-  // masks of a whole block ahead of the DFA chain costs ~100 VGPRs
-  __builtin_amdgcn_sched_barrier(0);
+template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x, const typename Step::Pre& pre,
+                                          uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
+  // StepTable: keep each word's work in place (hoisting the chain-independent
+  // newline masks of a whole block costs ~100 VGPRs). StepSheng8 wants the
+  // opposite: its state-independent LDS reads should run ahead of the chain.
+  if (Step::kKind == kStepTable || DGREP_SHENG_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);
   const uint32_t m = nl_mask(x);
-  const uint32_t s0 = dfa_step(tbl, s, x, 0x0c0c0400u);
-  const uint32_t s1 = dfa_step(tbl, s0, x, 0x0c0c0401u);
-  const uint32_t s2 = dfa_step(tbl, s1, x, 0x0c0c0402u);
-  const uint32_t s3 = dfa_step(tbl, s2, x, 0x0c0c0403u);
-  if (__builtin_expect((s0 == M) | (s1 == M) | (s2 == M) | (s3 == M), 0)) {
+  uint32_t s0, s1, s2, s3;
+  st.apply(pre, s, s0, s1, s2, s3);
+  if (__builtin_expect(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)), 0)) {
     // a '\n' in this word ends a matching line: resolve it exactly
     const uint64_t q0 = b.pos + 4u * J;
     const bool seen_w = r.seen || b.lastm != 0;
     const bool term_w = r.term || (b.past && b.lastm != 0);
     const int64_t prev_w = b.lastm ? int64_t(b.pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm)) : r.prev_nl;
-    uint32_t evm = uint32_t(s0 == M) | (uint32_t(s1 == M) << 1) | (uint32_t(s2 == M) << 2) | (uint32_t(s3 == M) << 3);
+    uint32_t evm = uint32_t(Step::is(s0, M)) | (uint32_t(Step::is(s1, M)) << 1) | (uint32_t(Step::is(s2, M)) << 2) |
+                   (uint32_t(Step::is(s3, M)) << 3);
     while (evm) {
       const uint32_t k = uint32_t(__builtin_ctz(evm));
       evm &= evm - 1;
@@ -141,8 +221,8 @@ __device__ __forceinline__ void word_step(const uint8_t* tbl, uint32_t M, uint32
   s = s3;
 }
 
-template <int E, bool DIRECT>
-__device__ __forceinline__ void run_block(const uint8_t* tbl, uint32_t M, const uint4 (&v)[4], uint64_t pos,
+template <class Step, int E, bool DIRECT>
+__device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[kBlk / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
   b.pos = pos;
@@ -152,13 +232,30 @@ __device__ __forceinline__ void run_block(const uint8_t* tbl, uint32_t M, const 
   b.lastm = 0;
   b.lastj = -1;
   uint32_t s = r.s;
-#define DG_W4(I)                                                           \
-  word_step<4 * I + 0, E, DIRECT>(tbl, M, v[I].x, s, b, r, emit);          \
-  word_step<4 * I + 1, E, DIRECT>(tbl, M, v[I].y, s, b, r, emit);          \
-  word_step<4 * I + 2, E, DIRECT>(tbl, M, v[I].z, s, b, r, emit);          \
-  word_step<4 * I + 3, E, DIRECT>(tbl, M, v[I].w, s, b, r, emit);
-  DG_W4(0) DG_W4(1) DG_W4(2) DG_W4(3)
-#undef DG_W4
+  // word j's state-independent work (Step::prep) is issued one word ahead
+  constexpr int NW = kBlk / 4;
+  uint32_t w[NW];
+#pragma unroll
+  for (int i = 0; i < kBlk / 16; ++i) {
+    w[4 * i + 0] = v[i].x;
+    w[4 * i + 1] = v[i].y;
+    w[4 * i + 2] = v[i].z;
+    w[4 * i + 3] = v[i].w;
+  }
+  typename Step::Pre pre = st.prep(w[0]);
+#define DG_W(J)                                                                         \
+  {                                                                                     \
+    const typename Step::Pre cur = pre;                                                 \
+    if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : (J)]);                   \
+    word_step<J>(st, M, w[J], cur, s, b, r, emit);                                      \
+  }
+  DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
+  DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
+#if DGREP_BLOCK == 128
+  DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
+  DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
+#endif
+#undef DG_W
   r.s = s;
   r.nl = b.nl0 + b.nlrun;
   if (b.lastm) {
@@ -168,24 +265,24 @@ __device__ __forceinline__ void run_block(const uint8_t* tbl, uint32_t M, const 
   }
 }
 
-__device__ __forceinline__ void load_block(uint4 (&v)[4], const uint8_t* p) {
+__device__ __forceinline__ void load_block(uint4 (&v)[kBlk / 16], const uint8_t* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = q[i];
+  for (int i = 0; i < kBlk / 16; ++i) v[i] = q[i];
 }
 
 // The last < 64 bytes of the split, one byte at a time, then the end of the
 // split closes the last owned line (strings.Split's final piece).
-template <int E, bool DIRECT>
-__device__ __forceinline__ void run_tail(const uint8_t* tbl, uint32_t M, const uint8_t* p, uint64_t pos, uint64_t avail, uint64_t C,
+template <class Step, int E, bool DIRECT>
+__device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8_t* p, uint64_t pos, uint64_t avail, uint64_t C,
                          LaneRun& r, uint32_t& nl_chunk, bool& snap, const Emitter<E, DIRECT>& emit) {
   for (; pos < avail; ++pos) {
     if (pos == C) { nl_chunk = r.nl; snap = true; }
     if (pos >= C && r.term) return;
     const uint32_t b = p[pos];
-    const uint32_t s1 = tbl[r.s * kRow + b];
+    const uint32_t s1 = st.byte(r.s, b);
     if (b == '\n') {
-      if (s1 == M && r.seen && !(pos >= C && r.term)) emit(r, pos, r.prev_nl + 1, r.nl);
+      if (Step::is(s1, M) && r.seen && !(pos >= C && r.term)) emit(r, pos, r.prev_nl + 1, r.nl);
       r.seen = true;
       ++r.nl;
       r.prev_nl = int64_t(pos);
@@ -193,14 +290,14 @@ __device__ __forceinline__ void run_tail(const uint8_t* tbl, uint32_t M, const u
     }
     r.s = s1;
   }
-  if (!r.term && r.seen && tbl[r.s * kRow + uint32_t('\n')] == M) emit(r, avail, r.prev_nl + 1, r.nl);
+  if (!r.term && r.seen && Step::is(st.byte(r.s, uint32_t('\n')), M)) emit(r, avail, r.prev_nl + 1, r.nl);
 }
 
 // Runs one lane (see file comment) over 64-byte blocks, prefetching the next
 // block while the current one is stepped (two register buffers, ping-pong).
 // Returns the number of '\n' inside the lane's own chunk [cs, cs + C).
-template <int C, int E, bool DIRECT>
-__device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const uint8_t* tbl, uint64_t cs, LaneRun& r,
+template <int C, class Step, int E, bool DIRECT>
+__device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
                                              const Emitter<E, DIRECT>& emit) {
   const uint32_t M = a.start_m;
   const uint64_t avail = cs < a.n ? a.n - cs : 0;
@@ -215,22 +312,22 @@ __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const uint8_t* t
   uint32_t nl_chunk = 0;
   bool snap = false;
   uint64_t pos = 0;
-  uint4 A[4], B[4];
-  if (avail >= 64) load_block(A, p);
+  uint4 A[kBlk / 16], B[kBlk / 16];
+  if (avail >= kBlk) load_block(A, p);
   for (;;) {
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
-    if (pos + 64 > avail) { run_tail<E, DIRECT>(tbl, M, p, pos, avail, C, r, nl_chunk, snap, emit); break; }
-    load_block(B, p + (pos + 128 <= avail ? pos + 64 : pos));  // prefetch (or a harmless re-read)
-    run_block<E, DIRECT>(tbl, M, A, pos, C, r, emit);
-    pos += 64;
+    if (pos + kBlk > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
+    load_block(B, p + (pos + 2 * kBlk <= avail ? pos + kBlk : pos));  // prefetch (or a harmless re-read)
+    run_block(st, M, A, pos, uint64_t(C), r, emit);
+    pos += kBlk;
 
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
-    if (pos + 64 > avail) { run_tail<E, DIRECT>(tbl, M, p, pos, avail, C, r, nl_chunk, snap, emit); break; }
-    load_block(A, p + (pos + 128 <= avail ? pos + 64 : pos));
-    run_block<E, DIRECT>(tbl, M, B, pos, C, r, emit);
-    pos += 64;
+    if (pos + kBlk > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
+    load_block(A, p + (pos + 2 * kBlk <= avail ? pos + kBlk : pos));
+    run_block(st, M, B, pos, uint64_t(C), r, emit);
+    pos += kBlk;
   }
   if (!snap) nl_chunk = r.nl;
   return nl_chunk;
@@ -246,7 +343,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-template <int C, int E, int TBL>
+// One wave = one tile of 64 chunks. Waves never synchronise with each other:
+// the tile's exclusive scans run on the wave's lanes (DPP/bpermute) and one
+// lane reserves the tile's staging range with a single atomic.
+template <class Step, int C, int E, int TBL>
 __global__ __launch_bounds__(kScanThreads) void scan_dfa8_kernel(ScanArgs a) {
   __shared__ ScanSmem<TBL, E> sm;
   const int tid = int(threadIdx.x);
@@ -254,141 +354,171 @@ __global__ __launch_bounds__(kScanThreads) void scan_dfa8_kernel(ScanArgs a) {
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
   __syncthreads();
 
+  const Step st = make_step<Step>(sm.tbl);
   uint32_t* slots = sm.slots + tid * E * 2;
-  uint32_t* scratch = sm.scratch;  // [0..3] nl wave sums, [4..7] match wave sums, [8..9] staging base
-  const int wave = tid >> 6;
   const int lane = tid & 63;
-
-  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
-    const uint64_t tile0 = t * uint64_t(kScanThreads) * uint64_t(C);
-    const uint64_t cs = tile0 + uint64_t(tid) * uint64_t(C);
+  const uint64_t waves = uint64_t(gridDim.x) * (kScanThreads / 64);
+  for (uint64_t t = uint64_t(blockIdx.x) * (kScanThreads / 64) + uint64_t(tid >> 6); t < a.ntiles; t += waves) {
+    const uint64_t cs = t * uint64_t(kTileLanes) * uint64_t(C) + uint64_t(lane) * uint64_t(C);
     LaneRun r;
     Emitter<E, false> em{&a, slots, cs, 0, 0};
-    const uint32_t nlc = run_lane<C, E, false>(a, sm.tbl, cs, r, em);
+    const uint32_t nlc = run_lane<C>(a, st, cs, r, em);
     const uint32_t nev = r.nev;
 
-    // tile-wide exclusive scans of (newlines, matching lines)
+    // tile-wide exclusive scans of (newlines, matching lines) across the wave
     const uint32_t nl_inc = wave_incl_scan(nlc);
     const uint32_t ev_inc = wave_incl_scan(nev);
-    if (lane == 63) {
-      scratch[wave] = nl_inc;
-      scratch[4 + wave] = ev_inc;
-    }
-    __syncthreads();
-    uint32_t nl_off = nl_inc - nlc, ev_off = ev_inc - nev;
-    uint32_t nl_tot = 0, ev_tot = 0;
-#pragma unroll
-    for (int w = 0; w < kScanThreads / 64; ++w) {
-      const uint32_t a_nl = scratch[w], a_ev = scratch[4 + w];
-      if (w < wave) { nl_off += a_nl; ev_off += a_ev; }
-      nl_tot += a_nl;
-      ev_tot += a_ev;
-    }
-    if (tid == 0) {
-      unsigned long long base = 0;
+    const uint32_t nl_tot = __shfl(nl_inc, 63, 64);
+    const uint32_t ev_tot = __shfl(ev_inc, 63, 64);
+    const uint32_t nl_off = nl_inc - nlc, ev_off = ev_inc - nev;
+    unsigned long long base = 0;
+    if (lane == 0) {
       if (ev_tot) base = atomicAdd(a.counter, (unsigned long long)ev_tot);
       TileInfo ti;
       ti.base = base;
       ti.count = ev_tot;
       ti.nl = nl_tot;
       a.tiles[t] = ti;
-      scratch[8] = uint32_t(base);
-      scratch[9] = uint32_t(base >> 32);
     }
-    __syncthreads();
-    if (ev_tot) {
-      const uint64_t base = (uint64_t(scratch[9]) << 32) | scratch[8];
-      const uint64_t o0 = base + ev_off;
-      if (nev <= uint32_t(E)) {
-        for (uint32_t k = 0; k < nev; ++k) {
-          const uint64_t o = o0 + k;
-          if (o < a.capacity) {
-            const uint32_t w0 = slots[k * 2 + 0];
-            StagedLine L;
-            L.start = cs + (w0 & 0xffffu);
-            L.len = slots[k * 2 + 1];
-            L.rel = nl_off + (w0 >> 16);
-            a.staging[o] = L;
-          }
-        }
-      } else {
-        // more matching lines than LDS slots: scan_overflow_kernel re-runs
-        // this lane and writes straight to its final staging positions
-        const unsigned long long k = atomicAdd(a.overflow_count, 1ull);
-        if (k < a.overflow_cap) {
-          OverflowLane ol;
-          ol.cs = cs;
-          ol.out_base = o0;
-          ol.nl_prefix = nl_off;
-          ol.pad = 0;
-          a.overflow[k] = ol;
+    if (ev_tot == 0) continue;  // wave-uniform
+    base = (uint64_t(uint32_t(__shfl(uint32_t(base >> 32), 0, 64))) << 32) | uint32_t(__shfl(uint32_t(base), 0, 64));
+    const uint64_t o0 = base + ev_off;
+    if (nev <= uint32_t(E)) {
+      for (uint32_t k = 0; k < nev; ++k) {
+        const uint64_t o = o0 + k;
+        if (o < a.capacity) {
+          const uint32_t w0 = slots[k * 2 + 0];
+          StagedLine L;
+          L.start = cs + (w0 & 0xffffu);
+          L.len = slots[k * 2 + 1];
+          L.rel = nl_off + (w0 >> 16);
+          a.staging[o] = L;
         }
       }
+    } else {
+      // more matching lines than LDS slots: scan_overflow_kernel re-runs
+      // this lane and writes straight to its final staging positions
+      const unsigned long long k = atomicAdd(a.overflow_count, 1ull);
+      if (k < a.overflow_cap) {
+        OverflowLane ol;
+        ol.cs = cs;
+        ol.out_base = o0;
+        ol.nl_prefix = nl_off;
+        ol.pad = 0;
+        a.overflow[k] = ol;
+      }
     }
-    __syncthreads();  // scratch/slots reuse by the next tile
   }
 }
 
 // Lanes that owned more matching lines than their LDS slots: one thread per
 // such lane runs it again in direct-write mode (rare: dense short matches).
-template <int C, int E, int TBL>
+template <class Step, int C, int E, int TBL>
 __global__ __launch_bounds__(64) void scan_overflow_kernel(ScanArgs a, uint64_t nover) {
   __shared__ ScanSmem<TBL, 1> sm;
   for (uint32_t i = threadIdx.x * 16u; i < a.table_bytes; i += 64 * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
   __syncthreads();
+  const Step st = make_step<Step>(sm.tbl);
   for (uint64_t k = uint64_t(blockIdx.x) * 64 + threadIdx.x; k < nover; k += uint64_t(gridDim.x) * 64) {
     const OverflowLane ol = a.overflow[k];
     LaneRun r;
     Emitter<E, true> ed{&a, nullptr, ol.cs, ol.out_base, ol.nl_prefix};
-    run_lane<C, E, true>(a, sm.tbl, ol.cs, r, ed);
+    run_lane<C>(a, st, ol.cs, r, ed);
   }
 }
 
-// Exclusive scans over the tiles (one workgroup): out_off = sum of counts of
-// earlier tiles, line_base = 1 + newlines of earlier tiles.
-__global__ __launch_bounds__(1024) void tile_scan_kernel(TileInfo* tiles, uint64_t ntiles, uint64_t* out_off,
-                                                         uint64_t* line_base) {
-  __shared__ uint64_t s_cnt[1024], s_nl[1024];
-  const uint64_t per = (ntiles + 1023) / 1024;
-  const uint64_t b = uint64_t(threadIdx.x) * per;
-  const uint64_t e = b + per < ntiles ? b + per : ntiles;
-  uint64_t c = 0, l = 0;
-  for (uint64_t i = b; i < e; ++i) { c += tiles[i].count; l += tiles[i].nl; }
-  s_cnt[threadIdx.x] = c;
-  s_nl[threadIdx.x] = l;
+// ---- ordering passes ------------------------------------------------------
+// Tiles append their lines to the staging buffer in atomic order; these passes
+// compute, per tile, its first output index (exclusive scan of counts) and the
+// 1-based number of its first line (1 + exclusive scan of newline counts), then
+// copy every tile's lines to their final place in split order.
+constexpr int kOrdThreads = 256;
+constexpr int kOrdPerThread = 16;
+constexpr int kOrdTiles = kOrdThreads * kOrdPerThread;  // tiles per ordering block
+
+__device__ __forceinline__ void block_excl_scan2(uint64_t& a, uint64_t& b, uint64_t* sh_a, uint64_t* sh_b,
+                                                 uint64_t& tot_a, uint64_t& tot_b) {
+  const int t = int(threadIdx.x);
+  sh_a[t] = a;
+  sh_b[t] = b;
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    uint64_t tc = 0, tl = 0;
-    if (int(threadIdx.x) >= d) { tc = s_cnt[threadIdx.x - d]; tl = s_nl[threadIdx.x - d]; }
+  for (int d = 1; d < kOrdThreads; d <<= 1) {
+    uint64_t xa = 0, xb = 0;
+    if (t >= d) { xa = sh_a[t - d]; xb = sh_b[t - d]; }
     __syncthreads();
-    s_cnt[threadIdx.x] += tc;
-    s_nl[threadIdx.x] += tl;
+    sh_a[t] += xa;
+    sh_b[t] += xb;
     __syncthreads();
   }
-  c = s_cnt[threadIdx.x] - c;
-  l = s_nl[threadIdx.x] - l;
-  for (uint64_t i = b; i < e; ++i) {
-    out_off[i] = c;
-    line_base[i] = l + 1;
-    c += tiles[i].count;
-    l += tiles[i].nl;
-  }
-  if (threadIdx.x == 1023) {
-    out_off[ntiles] = s_cnt[1023];
-    line_base[ntiles] = s_nl[1023] + 1;
+  tot_a = sh_a[kOrdThreads - 1];
+  tot_b = sh_b[kOrdThreads - 1];
+  a = sh_a[t] - a;
+  b = sh_b[t] - b;
+  __syncthreads();
+}
+
+// pass 1: per ordering block, the sums of its tiles' counts and newlines
+__global__ __launch_bounds__(kOrdThreads) void tile_reduce_kernel(const TileInfo* tiles, uint64_t ntiles,
+                                                                   uint64_t* blk_cnt, uint64_t* blk_nl) {
+  __shared__ uint64_t sa[kOrdThreads], sb[kOrdThreads];
+  const uint64_t t0 = uint64_t(blockIdx.x) * kOrdTiles + uint64_t(threadIdx.x) * kOrdPerThread;
+  uint64_t c = 0, l = 0;
+  for (int i = 0; i < kOrdPerThread; ++i)
+    if (t0 + i < ntiles) { c += tiles[t0 + i].count; l += tiles[t0 + i].nl; }
+  uint64_t tc, tl;
+  block_excl_scan2(c, l, sa, sb, tc, tl);
+  if (threadIdx.x == 0) { blk_cnt[blockIdx.x] = tc; blk_nl[blockIdx.x] = tl; }
+}
+
+// pass 2: exclusive scan over the ordering blocks (one workgroup, any count)
+__global__ __launch_bounds__(kOrdThreads) void block_scan_kernel(uint64_t* blk_cnt, uint64_t* blk_nl, uint64_t nblk) {
+  __shared__ uint64_t sa[kOrdThreads], sb[kOrdThreads];
+  uint64_t carry_c = 0, carry_l = 0;
+  for (uint64_t b0 = 0; b0 < nblk; b0 += kOrdThreads) {
+    const uint64_t i = b0 + threadIdx.x;
+    uint64_t c = i < nblk ? blk_cnt[i] : 0, l = i < nblk ? blk_nl[i] : 0;
+    uint64_t tc, tl;
+    block_excl_scan2(c, l, sa, sb, tc, tl);
+    if (i < nblk) { blk_cnt[i] = carry_c + c; blk_nl[i] = carry_l + l; }
+    carry_c += tc;
+    carry_l += tl;
   }
 }
 
-// Tile-ordered copy of the staged lines into the result arrays (SoA).
+// pass 3: per tile, its output offset and first line number
+__global__ __launch_bounds__(kOrdThreads) void tile_offsets_kernel(const TileInfo* tiles, uint64_t ntiles,
+                                                                    const uint64_t* blk_cnt, const uint64_t* blk_nl,
+                                                                    uint64_t* out_off, uint64_t* line_base) {
+  __shared__ uint64_t sa[kOrdThreads], sb[kOrdThreads];
+  const uint64_t t0 = uint64_t(blockIdx.x) * kOrdTiles + uint64_t(threadIdx.x) * kOrdPerThread;
+  uint64_t c = 0, l = 0;
+  for (int i = 0; i < kOrdPerThread; ++i)
+    if (t0 + i < ntiles) { c += tiles[t0 + i].count; l += tiles[t0 + i].nl; }
+  uint64_t tc, tl;
+  block_excl_scan2(c, l, sa, sb, tc, tl);
+  c += blk_cnt[blockIdx.x];
+  l += blk_nl[blockIdx.x];
+  for (int i = 0; i < kOrdPerThread; ++i) {
+    if (t0 + i >= ntiles) break;
+    out_off[t0 + i] = c;
+    line_base[t0 + i] = l + 1;
+    c += tiles[t0 + i].count;
+    l += tiles[t0 + i].nl;
+  }
+}
+
+// pass 4: one wave per tile copies its staged lines to their final slots (SoA)
 __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles, const StagedLine* staging,
                                                           uint64_t ntiles, const uint64_t* out_off,
                                                           const uint64_t* line_base, uint64_t capacity,
                                                           uint64_t* line_no, uint64_t* start, uint32_t* len) {
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  const uint64_t waves = uint64_t(gridDim.x) * 4;
+  for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles; t += waves) {
     const TileInfo ti = tiles[t];
+    if (ti.count == 0) continue;
     const uint64_t o = out_off[t], lb = line_base[t];
-    for (uint32_t k = threadIdx.x; k < ti.count; k += blockDim.x) {
+    for (uint32_t k = threadIdx.x & 63; k < ti.count; k += 64) {
       const uint64_t src = ti.base + k, dst = o + k;
       if (src < capacity && dst < capacity) {
         const StagedLine L = staging[src];
@@ -402,66 +532,87 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
 
 // ---- host-side launchers (called from dgrep_runtime.cpp) ----------------
 
-constexpr int kChunk = 1024;  // bytes per lane chunk (multiple of 128)
-constexpr int kSlots = 8;     // LDS slots per lane for matching lines
+constexpr int kChunk = DGREP_CHUNK;  // bytes per lane chunk (multiple of 128)
+constexpr int kSlots = DGREP_SLOTS;  // LDS slots per lane for matching lines
 
-uint64_t scan_tile_bytes() { return uint64_t(kScanThreads) * kChunk; }
+uint64_t scan_tile_bytes() { return uint64_t(kTileLanes) * kChunk; }
 uint32_t scan_table_row() { return kRow; }
 
 namespace {
-template <int TBL>
+template <class Step, int TBL>
 hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((scan_dfa8_kernel<kChunk, kSlots, TBL>), dim3(grid), dim3(kScanThreads), 0, stream, a);
+  hipLaunchKernelGGL((scan_dfa8_kernel<Step, kChunk, kSlots, TBL>), dim3(grid), dim3(kScanThreads), 0, stream, a);
   return hipGetLastError();
 }
-template <int TBL>
+template <class Step, int TBL>
 hipError_t overflow_t(const ScanArgs& a, uint64_t nover, hipStream_t stream) {
   int grid = int((nover + 63) / 64);
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL((scan_overflow_kernel<kChunk, kSlots, TBL>), dim3(grid), dim3(64), 0, stream, a, nover);
+  hipLaunchKernelGGL((scan_overflow_kernel<Step, kChunk, kSlots, TBL>), dim3(grid), dim3(64), 0, stream, a, nover);
   return hipGetLastError();
 }
-template <int TBL>
+template <class Step, int TBL>
 hipError_t occ_t(int* b) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<kChunk, kSlots, TBL>, kScanThreads, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, kChunk, kSlots, TBL>, kScanThreads,
+                                                      0);
 }
+
+// One switch for every entry point: stepper by kind, LDS image by size.
+template <class Op>
+hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
+  if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
+  if (table_bytes <= 16 * kRow) return op.template run<StepTable, 16 * kRow>();
+  if (table_bytes <= 32 * kRow) return op.template run<StepTable, 32 * kRow>();
+  if (table_bytes <= 64 * kRow) return op.template run<StepTable, 64 * kRow>();
+  if (table_bytes <= 128 * kRow) return op.template run<StepTable, 128 * kRow>();
+  return op.template run<StepTable, 256 * kRow>();
+}
+struct OccOp {
+  int* b;
+  template <class S, int T>
+  hipError_t run() const { return occ_t<S, T>(b); }
+};
+struct LaunchOp {
+  const ScanArgs* a;
+  int grid;
+  hipStream_t s;
+  template <class S, int T>
+  hipError_t run() const { return launch_t<S, T>(*a, grid, s); }
+};
+struct OverflowOp {
+  const ScanArgs* a;
+  uint64_t n;
+  hipStream_t s;
+  template <class S, int T>
+  hipError_t run() const { return overflow_t<S, T>(*a, n, s); }
+};
 }  // namespace
 
-// variants by table size: up to 16, 32, 64, 128, 256 states
-hipError_t scan_dfa8_occupancy(uint32_t table_bytes, int* b) {
-  if (table_bytes <= 16 * kRow) return occ_t<16 * kRow>(b);
-  if (table_bytes <= 32 * kRow) return occ_t<32 * kRow>(b);
-  if (table_bytes <= 64 * kRow) return occ_t<64 * kRow>(b);
-  if (table_bytes <= 128 * kRow) return occ_t<128 * kRow>(b);
-  return occ_t<256 * kRow>(b);
+hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {
+  return dispatch(kind, table_bytes, OccOp{blocks_per_cu});
+}
+hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream) {
+  return dispatch(kind, a.table_bytes, LaunchOp{&a, grid, stream});
+}
+hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStream_t stream) {
+  return dispatch(kind, a.table_bytes, OverflowOp{&a, nover, stream});
 }
 
-hipError_t scan_dfa8(const ScanArgs& a, int grid, hipStream_t stream) {
-  if (a.table_bytes <= 16 * kRow) return launch_t<16 * kRow>(a, grid, stream);
-  if (a.table_bytes <= 32 * kRow) return launch_t<32 * kRow>(a, grid, stream);
-  if (a.table_bytes <= 64 * kRow) return launch_t<64 * kRow>(a, grid, stream);
-  if (a.table_bytes <= 128 * kRow) return launch_t<128 * kRow>(a, grid, stream);
-  return launch_t<256 * kRow>(a, grid, stream);
-}
+uint64_t order_blocks(uint64_t ntiles) { return (ntiles + kOrdTiles - 1) / kOrdTiles; }
 
-hipError_t scan_dfa8_overflow(const ScanArgs& a, uint64_t nover, hipStream_t stream) {
-  if (a.table_bytes <= 16 * kRow) return overflow_t<16 * kRow>(a, nover, stream);
-  if (a.table_bytes <= 32 * kRow) return overflow_t<32 * kRow>(a, nover, stream);
-  if (a.table_bytes <= 64 * kRow) return overflow_t<64 * kRow>(a, nover, stream);
-  if (a.table_bytes <= 128 * kRow) return overflow_t<128 * kRow>(a, nover, stream);
-  return overflow_t<256 * kRow>(a, nover, stream);
-}
-
-hipError_t tile_scan(TileInfo* tiles, uint64_t ntiles, uint64_t* out_off, uint64_t* line_base, hipStream_t stream) {
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, stream, tiles, ntiles, out_off, line_base);
-  return hipGetLastError();
-}
-
-hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, const uint64_t* out_off,
-                       const uint64_t* line_base, uint64_t capacity, uint64_t* line_no, uint64_t* start,
+// out_off / line_base: ntiles entries; blk: 2 * order_blocks(ntiles) scratch
+hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
+                       uint64_t* line_base, uint64_t* blk, uint64_t capacity, uint64_t* line_no, uint64_t* start,
                        uint32_t* len, hipStream_t stream) {
-  int grid = int(ntiles < 4096 ? ntiles : 4096);
-  if (grid < 1) grid = 1;
+  const uint64_t nblk = order_blocks(ntiles);
+  uint64_t* blk_cnt = blk;
+  uint64_t* blk_nl = blk + nblk;
+  hipLaunchKernelGGL(tile_reduce_kernel, dim3(nblk), dim3(kOrdThreads), 0, stream, tiles, ntiles, blk_cnt, blk_nl);
+  hipLaunchKernelGGL(block_scan_kernel, dim3(1), dim3(kOrdThreads), 0, stream, blk_cnt, blk_nl, nblk);
+  hipLaunchKernelGGL(tile_offsets_kernel, dim3(nblk), dim3(kOrdThreads), 0, stream, tiles, ntiles, blk_cnt, blk_nl,
+                     out_off, line_base);
+  uint64_t grid = (ntiles + 3) / 4;
+  if (grid > 16384) grid = 16384;
   hipLaunchKernelGGL(order_lines_kernel, dim3(grid), dim3(256), 0, stream, tiles, staging, ntiles, out_off,
                      line_base, capacity, line_no, start, len);
   return hipGetLastError();

@@ -22,12 +22,12 @@ namespace dgrep {
 // scan_dfa.hip
 uint64_t scan_tile_bytes();
 uint32_t scan_table_row();
-hipError_t scan_dfa8_occupancy(uint32_t table_bytes, int* blocks_per_cu);
-hipError_t scan_dfa8(const ScanArgs& a, int grid, hipStream_t stream);
-hipError_t scan_dfa8_overflow(const ScanArgs& a, uint64_t nover, hipStream_t stream);
-hipError_t tile_scan(TileInfo* tiles, uint64_t ntiles, uint64_t* out_off, uint64_t* line_base, hipStream_t stream);
-hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, const uint64_t* out_off,
-                       const uint64_t* line_base, uint64_t capacity, uint64_t* line_no, uint64_t* start,
+hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu);
+hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
+hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStream_t stream);
+uint64_t order_blocks(uint64_t ntiles);
+hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
+                       uint64_t* line_base, uint64_t* blk, uint64_t capacity, uint64_t* line_no, uint64_t* start,
                        uint32_t* len, hipStream_t stream);
 }  // namespace dgrep
 
@@ -44,15 +44,17 @@ struct dgrep_ctx {
   bool loaded = false;
   uint32_t flags = 0, nstates = 0, start = 0, start_m = 0;
   bool empty_line_matches = false;
-  uint8_t* d_table = nullptr;  // u8 [state][byte], row stride scan_table_row()
+  uint8_t* d_table = nullptr;  // stepper image (see dgrep_load_dfa)
   uint32_t table_bytes = 0;
+  int step_kind = kStepTable;
   int blocks_per_cu = 1;
 
   // per-scan scratch (grown on demand, reused)
   TileInfo* d_tiles = nullptr;
   uint64_t* d_out_off = nullptr;
   uint64_t* d_line_base = nullptr;
-  uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0;
+  uint64_t* d_blk = nullptr;
+  uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0, blk_cap = 0;
   StagedLine* d_staging = nullptr;
   uint64_t staging_cap = 0;
   // device counters: [0] staging append counter, [1] overflow lanes, [2] status bits
@@ -123,7 +125,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -162,12 +164,23 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
              " states; this build scans DFAs of at most 256 states (LDS-resident u8 table)";
     return DGREP_E_UNSUPPORTED;
   }
-  // expand byte classes into the kernel's LDS image: row s (stride
-  // scan_table_row() = 260, bank-staggered) holds trans[s][class(b)] at byte b
-  const size_t row = scan_table_row();
-  std::vector<uint8_t> t((size_t(h.nstates) * row + 15) & ~size_t(15), 0);
-  for (uint32_t s = 0; s < h.nstates; ++s)
-    for (int b = 0; b < 256; ++b) t[size_t(s) * row + size_t(b)] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
+  // expand byte classes into the kernel's LDS image
+  std::vector<uint8_t> t;
+  if (h.nstates <= 8) {
+    // StepSheng8: V[b] = 8 bytes, byte s = next state of s on input byte b
+    c->step_kind = kStepSheng8;
+    t.assign(256 * 8, 0);
+    for (int b = 0; b < 256; ++b)
+      for (uint32_t s = 0; s < h.nstates; ++s) t[size_t(b) * 8 + s] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
+  } else {
+    // StepTable: row s (stride scan_table_row() = 260, bank-staggered) holds
+    // trans[s][class(b)] at byte b
+    c->step_kind = kStepTable;
+    const size_t row = scan_table_row();
+    t.assign((size_t(h.nstates) * row + 15) & ~size_t(15), 0);
+    for (uint32_t s = 0; s < h.nstates; ++s)
+      for (int b = 0; b < 256; ++b) t[size_t(s) * row + size_t(b)] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
+  }
   if (c->d_table) HIPCHK(hipFree(c->d_table));
   c->d_table = nullptr;
   c->table_bytes = uint32_t(t.size());
@@ -179,7 +192,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->start_m = h.start_m;
   c->empty_line_matches = trans[size_t(h.start) * h.nclasses + h.byte_class[uint8_t('\n')]] == h.start_m;
   int bpc = 0;
-  HIPCHK(scan_dfa8_occupancy(c->table_bytes, &bpc));
+  HIPCHK(scan_dfa_occupancy(c->step_kind, c->table_bytes, &bpc));
   c->blocks_per_cu = std::max(1, bpc);
   c->loaded = true;
   return DGREP_OK;
@@ -215,6 +228,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   if ((rc = grow(c, &c->d_tiles, &c->tiles_cap, ntiles)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_out_off, &c->off_cap, ntiles + 1)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_line_base, &c->lb_cap, ntiles + 1)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_blk, &c->blk_cap, 2 * order_blocks(ntiles) + 2)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_staging, &c->staging_cap, capacity)) != DGREP_OK) return rc;
 
   if (!c->d_overflow && (rc = grow(c, &c->d_overflow, &c->overflow_cap, 1u << 16)) != DGREP_OK) return rc;
@@ -242,7 +256,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     a.overflow_cap = c->overflow_cap;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
-    HIPCHK(scan_dfa8(a, grid, c->stream));
+    HIPCHK(scan_dfa(c->step_kind, a, grid, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     HIPCHK(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -256,12 +270,11 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     c->err = "a matching line is longer than 4 GiB (uint32 length in dgrep_result)";
     return DGREP_E_UNSUPPORTED;
   }
-  if (ctr[1] && total <= capacity) HIPCHK(scan_dfa8_overflow(a, ctr[1], c->stream));
+  if (ctr[1] && total <= capacity) HIPCHK(scan_dfa_overflow(c->step_kind, a, ctr[1], c->stream));
   *count = total;
   if (total == 0 || total > capacity) return DGREP_OK;
-  HIPCHK(tile_scan(c->d_tiles, ntiles, c->d_out_off, c->d_line_base, c->stream));
-  HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, capacity, d_line, d_start, d_len,
-                     c->stream));
+  HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->d_blk, capacity, d_line,
+                     d_start, d_len, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return DGREP_OK;
 }

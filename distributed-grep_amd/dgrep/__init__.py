@@ -32,7 +32,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdgrep.so")
+LIB_PATH = os.environ.get("DGREP_LIB") or os.path.join(os.path.dirname(_HERE), "libdgrep.so")
 
 DGREP_OK = 0
 DGREP_E_INVALID = 1

@@ -1,0 +1,76 @@
+"""C ABI checks that need no GPU: libdgrep.so loads, exports every function
+include/*.h declares, validates blobs, and fails loudly (no CPU fallback) when
+no GPU is present."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import dgrep
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in ("dgrep.h",):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"\b(?:int|void|const char\*)\s+(dgrep_\w+)\s*\(", src):
+            names.add(m.group(1))
+    return names
+
+
+def test_exports_every_declared_symbol():
+    L = dgrep.lib()
+    declared = _declared()
+    assert len(declared) >= 15
+    missing = [n for n in declared if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(dgrep.EXPORTS) <= declared
+
+
+def test_compile_errors_and_unsupported():
+    with pytest.raises(dgrep.UnsupportedPattern):
+        dgrep.CompiledPattern("\\p{Greek}")
+    cp = dgrep.CompiledPattern("(")
+    assert cp.go_syntax_error
+    assert "syntax" in cp.message
+
+
+def test_blob_validation():
+    L = dgrep.lib()
+    cp = dgrep.CompiledPattern("error")
+    info = dgrep._BlobInfo()
+    assert L.dgrep_blob_info_get(cp.blob, len(cp.blob), ctypes.byref(info)) == dgrep.DGREP_OK
+    assert (info.nstates, info.start, info.start_m) == (cp.nstates, 0, 1)
+    bad = bytearray(cp.blob)
+    bad[0] ^= 0xFF
+    assert L.dgrep_blob_info_get(bytes(bad), len(bad), ctypes.byref(info)) == dgrep.DGREP_E_INVALID
+    assert L.dgrep_blob_info_get(cp.blob, len(cp.blob) - 4, ctypes.byref(info)) == dgrep.DGREP_E_INVALID
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(dgrep.DgrepError):
+        dgrep.Context(0)
+    dgrep.set_pattern("error")
+    with pytest.raises(dgrep.DgrepError):
+        dgrep.Map("f", "an error\n")
+
+
+def test_synth_host_deterministic_and_shaped():
+    a = dgrep.synth_corpus_host(1 << 16, 5, 0)
+    b = dgrep.synth_corpus_host(1 << 16, 5, 0)
+    assert a == b and len(a) == 1 << 16
+    assert a.endswith(b"\n")
+    lines = a.split(b"\n")[:-1]
+    assert all(40 <= len(x) + 1 <= 200 for x in lines)
+    assert all(32 <= c < 127 for x in lines for c in x)
+    assert dgrep.synth_corpus_host(1 << 16, 6, 0) != a
+    kws = dgrep.synth_keywords(4, 1000)
+    assert len(set(kws)) > 990 and all(5 <= len(k) <= 12 and k.isalpha() and k.islower() for k in kws)

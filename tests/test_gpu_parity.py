@@ -81,13 +81,14 @@ def test_random_small(gpu_ctx, pattern):
         _check(gpu_ctx, pattern, data)
 
 
-@pytest.mark.parametrize("size", [1, 63, 64, 1023, 1024, 1025, 262143, 262144, 262145, 3 * 262144 + 17])
+@pytest.mark.parametrize("size", [1, 63, 64, 1023, 1024, 1025, 2048, 2049, 131071, 131072, 131073, 262143, 262144,
+                                  262145, 3 * 262144 + 17])
 def test_tile_and_chunk_boundaries(gpu_ctx, size):
     import dgrep
 
     data = bytearray(dgrep.synth_corpus_host(size, 11, 0))
     # force lines that end / start exactly at chunk and tile edges
-    for edge in (1023, 1024, 2047, 262143, 262144):
+    for edge in (1023, 1024, 2047, 2048, 4095, 4096, 65535, 65536, 131071, 131072, 262143, 262144):
         if edge < size:
             data[edge] = 0x0A
     data = bytes(data)

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kT) void lane_kernel(const uint8_t* __restrict__ da
       }
     }
   }
-  if (acc == 0x12345678u && s == 77) out[0] = acc;  // keep live
+  out[2 + blockIdx.x * kT + threadIdx.x] = acc ^ s;  // keep live
 }
 
 // NS independent streams per lane: lane handles chunks tid and tid + kT*k
@@ -153,7 +153,114 @@ __global__ __launch_bounds__(kT) void multi_kernel(const uint8_t* __restrict__ d
   uint32_t z = acc;
 #pragma unroll
   for (int k = 0; k < NS; ++k) z ^= s[k];
-  if (z == 0x12345678u) out[0] = z;
+  out[2 + blockIdx.x * kT + threadIdx.x] = z;
+}
+
+// Sheng-style DFA for <= 8 states: per input byte b an 8-byte vector
+// V[b][s] = next state; one v_perm_b32 per byte is the whole dependent chain,
+// and the LDS reads of V[b] do not depend on the state (ILP).
+template <int MODE>
+__global__ __launch_bounds__(kT) void sheng_kernel(const uint8_t* __restrict__ data, uint64_t n, int C,
+                                                   const uint2* vtab, uint32_t* out, uint32_t M) {
+  __shared__ uint2 V[256];
+  for (int i = threadIdx.x; i < 256; i += kT) V[i] = vtab[i];
+  __syncthreads();
+  const uint64_t ntiles = n / (uint64_t(kT) * C);
+  uint32_t acc = 0, s = 0;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint4* p = reinterpret_cast<const uint4*>(data + t * uint64_t(kT) * C + uint64_t(threadIdx.x) * C);
+    const int nb = C / 64;
+    uint4 A[4], B[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A[i] = p[i];
+    for (int b = 0; b < nb; ++b) {
+      const int nx = b + 1 < nb ? b + 1 : b;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) B[i] = p[nx * 4 + i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t w4[4] = {A[i].x, A[i].y, A[i].z, A[i].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t x = w4[q];
+          const uint2 m0 = V[x & 0xff], m1 = V[(x >> 8) & 0xff], m2 = V[(x >> 16) & 0xff], m3 = V[x >> 24];
+          const uint32_t s0 = __builtin_amdgcn_perm(m0.y, m0.x, s);
+          const uint32_t s1 = __builtin_amdgcn_perm(m1.y, m1.x, s0);
+          const uint32_t s2 = __builtin_amdgcn_perm(m2.y, m2.x, s1);
+          const uint32_t s3 = __builtin_amdgcn_perm(m3.y, m3.x, s2);
+          if (MODE >= 2) acc += __popc(nl_mask(x));
+          if (MODE >= 3) {
+            if (__builtin_expect(((s0 & 0xff) == M) | ((s1 & 0xff) == M) | ((s2 & 0xff) == M) | ((s3 & 0xff) == M), 0))
+              atomicAdd(out + 1, 1u);
+          }
+          s = s3;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) A[i] = B[i];
+    }
+  }
+  out[2 + blockIdx.x * kT + threadIdx.x] = acc ^ s;
+}
+
+template <int NS>
+__global__ __launch_bounds__(kT) void sheng_multi(const uint8_t* __restrict__ data, uint64_t n, int C,
+                                                  const uint2* vtab, uint32_t* out, uint32_t M) {
+  __shared__ uint2 V[256];
+  for (int i = threadIdx.x; i < 256; i += kT) V[i] = vtab[i];
+  __syncthreads();
+  const uint64_t tile = uint64_t(kT) * C * NS;
+  const uint64_t ntiles = n / tile;
+  uint32_t acc = 0;
+  uint32_t s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) s[k] = 0;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint4* p[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      p[k] = reinterpret_cast<const uint4*>(data + t * tile + (uint64_t(k) * kT + threadIdx.x) * C);
+    const int nb = C / 64;
+    uint4 A[NS][4], B[NS][4];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) A[k][i] = p[k][i];
+    for (int b = 0; b < nb; ++b) {
+      const int nx = b + 1 < nb ? b + 1 : b;
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) B[k][i] = p[k][nx * 4 + i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int k = 0; k < NS; ++k) {
+            const uint32_t x = q == 0 ? A[k][i].x : q == 1 ? A[k][i].y : q == 2 ? A[k][i].z : A[k][i].w;
+            const uint2 m0 = V[x & 0xff], m1 = V[(x >> 8) & 0xff], m2 = V[(x >> 16) & 0xff], m3 = V[x >> 24];
+            const uint32_t s0 = __builtin_amdgcn_perm(m0.y, m0.x, s[k]);
+            const uint32_t s1 = __builtin_amdgcn_perm(m1.y, m1.x, s0);
+            const uint32_t s2 = __builtin_amdgcn_perm(m2.y, m2.x, s1);
+            const uint32_t s3 = __builtin_amdgcn_perm(m3.y, m3.x, s2);
+            acc += __popc(nl_mask(x));
+            if (__builtin_expect(((s0 & 0xff) == M) | ((s1 & 0xff) == M) | ((s2 & 0xff) == M) | ((s3 & 0xff) == M), 0))
+              atomicAdd(out + 1, 1u);
+            s[k] = s3;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A[k][i] = B[k][i];
+    }
+  }
+  uint32_t z = acc;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) z ^= s[k];
+  out[2 + blockIdx.x * kT + threadIdx.x] = z;
 }
 
 __global__ void coalesced_kernel(const uint4* __restrict__ d, uint64_t n16, uint32_t* out) {
@@ -162,7 +269,7 @@ __global__ void coalesced_kernel(const uint4* __restrict__ d, uint64_t n16, uint
     uint4 v = d[i];
     acc ^= v.x ^ v.y ^ v.z ^ v.w;
   }
-  if (acc == 0x12345678u) out[0] = acc;
+  out[2 + blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
 __global__ void fill_kernel(uint8_t* d, uint64_t n) {
@@ -201,7 +308,7 @@ int main(int argc, char** argv) {
   uint32_t* out;
   uint8_t* tbl;
   CHK(hipMalloc(&d, n + 4096));
-  CHK(hipMalloc(&out, 64));
+  CHK(hipMalloc(&out, (2 + 8192 * 256) * 4));
   CHK(hipMalloc(&tbl, 16 * kRow));
   fill_kernel<<<4096, 256>>>(d, n);
   // 'error' DFA-like table: 7 states, mostly back to 0
@@ -217,11 +324,17 @@ int main(int argc, char** argv) {
     }
   for (int b = 0; b < 256; ++b) h[6 * kRow + b] = h[0 * kRow + b];
   CHK(hipMemcpy(tbl, h.data(), h.size(), hipMemcpyHostToDevice));
+  std::vector<uint8_t> vt(256 * 8, 0);
+  for (int b = 0; b < 256; ++b)
+    for (int st = 0; st < 8; ++st) vt[b * 8 + st] = st < 7 ? h[st * kRow + b] : 0;
+  uint2* vtab;
+  CHK(hipMalloc(&vtab, 256 * 8));
+  CHK(hipMemcpy(vtab, vt.data(), vt.size(), hipMemcpyHostToDevice));
   CHK(hipDeviceSynchronize());
   const uint32_t M = 6;
   auto gbs = [&](float ms) { return double(n) / (ms * 1e-3) / 1e9; };
   const int reps = 5;
-  for (int occ : {4, 5, 6, 8}) {
+  for (int occ : {4, 6, 8}) {
     const int grid = cus * occ;
     printf("--- grid %d WGs (%d per CU), C=%d, n=%.1f GiB\n", grid, occ, C, n / double(1 << 30));
     float ms;
@@ -239,6 +352,12 @@ int main(int argc, char** argv) {
     printf("V2  + newline SWAR   %8.1f GB/s\n", gbs(ms));
     ms = timeit([&] { lane_kernel<3, 1><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
     printf("V3  + event branch   %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { sheng_kernel<1><<<grid, kT>>>(d, n, C, vtab, out, M); }, reps);
+    printf("V5  sheng8 DFA       %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { sheng_kernel<3><<<grid, kT>>>(d, n, C, vtab, out, M); }, reps);
+    printf("V5b sheng8+nl+event  %8.1f GB/s\n", gbs(ms));
+    ms = timeit([&] { sheng_multi<2><<<grid, kT>>>(d, n, C, vtab, out, M); }, reps);
+    printf("V6  sheng8 x2 streams%8.1f GB/s\n", gbs(ms));
     ms = timeit([&] { multi_kernel<2><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);
     printf("V4  V2 x2 streams    %8.1f GB/s\n", gbs(ms));
     ms = timeit([&] { multi_kernel<4><<<grid, kT>>>(d, n, C, tbl, out, M); }, reps);

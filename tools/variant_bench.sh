@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B the tuning variants built by `make -C distributed-grep_amd variants` (run ON the GPU box).
+#   tools/variant_bench.sh <workload> [variant ...]
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+WL=${1:-c2}; shift || true
+VARS=${@:-base b128 c4k c4kb128 c1k c1kb128}
+for v in $VARS; do
+  for rep in 1 2; do
+    out=$(DGREP_LIB=$R/distributed-grep_amd/variants/libdgrep_$v.so timeout -k 10 180 python3 $R/bench.py --workload $WL --steps 6 --warmup 2 --no-cpu-baseline --verify-windows 1 2>/dev/null) || { echo "$v FAILED"; exit 1; }
+    echo "$v rep$rep $(echo "$out" | python3 -c 'import json,sys; d=json.load(sys.stdin); r=d["roofline"]; print("value=%.0f kernel=%.0f GB/s frac=%.3f kms=%.3f verified=%s" % (d["value"], r["achieved"], r["frac"], r["kernel_ms_avg"], d["config"]["verified_windows"]))')"
+  done
+done
