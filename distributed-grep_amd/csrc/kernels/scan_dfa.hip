@@ -40,15 +40,31 @@
 
 #include "scan_common.h"
 
-// build-time tuning knobs (defaults are the shipped configuration)
-#ifndef DGREP_CHUNK
-#define DGREP_CHUNK 4096
+// build-time tuning knobs, per stepper (defaults are the shipped
+// configuration, chosen by tools/variant_bench.sh on MI355X):
+//   CHUNK  bytes per lane chunk (multiple of BLOCK)
+//   SLOTS  LDS slots per lane for matching lines
+//   BLOCK  bytes per lane per register load block (64 or 128)
+// The Sheng stepper's chain is VALU-only, so it likes long chunks and big
+// blocks; the table stepper's chain waits on LDS and its 2-6 waves/SIMD need
+// the VGPRs a 128-byte block would take.
+#ifndef DGREP_SHENG_CHUNK
+#define DGREP_SHENG_CHUNK 4096
 #endif
-#ifndef DGREP_SLOTS
-#define DGREP_SLOTS 24
+#ifndef DGREP_SHENG_SLOTS
+#define DGREP_SHENG_SLOTS 24
 #endif
-#ifndef DGREP_BLOCK
-#define DGREP_BLOCK 128  // bytes per lane per load block (64 or 128)
+#ifndef DGREP_SHENG_BLOCK
+#define DGREP_SHENG_BLOCK 128
+#endif
+#ifndef DGREP_TABLE_CHUNK
+#define DGREP_TABLE_CHUNK 1024
+#endif
+#ifndef DGREP_TABLE_SLOTS
+#define DGREP_TABLE_SLOTS 8
+#endif
+#ifndef DGREP_TABLE_BLOCK
+#define DGREP_TABLE_BLOCK 64
 #endif
 #ifndef DGREP_SHENG_SCHED_BARRIER
 #define DGREP_SHENG_SCHED_BARRIER 0
@@ -56,8 +72,6 @@
 
 namespace dgrep {
 
-constexpr int kBlk = DGREP_BLOCK;
-static_assert(kBlk == 64 || kBlk == 128, "DGREP_BLOCK must be 64 or 128");
 
 __device__ __forceinline__ uint32_t nl_mask(uint32_t w) {
   // exact per-byte zero test of w ^ '\n\n\n\n': bit 7 of byte k set iff byte k == '\n'
@@ -137,6 +151,21 @@ template <>
 __device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds) {
   return StepSheng8{reinterpret_cast<const uint2*>(lds)};
 }
+
+template <class Step>
+struct Tune;
+template <>
+struct Tune<StepSheng8> {
+  static constexpr int C = DGREP_SHENG_CHUNK, E = DGREP_SHENG_SLOTS, B = DGREP_SHENG_BLOCK;
+};
+template <>
+struct Tune<StepTable> {
+  static constexpr int C = DGREP_TABLE_CHUNK, E = DGREP_TABLE_SLOTS, B = DGREP_TABLE_BLOCK;
+};
+static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block must be 64 or 128 bytes");
+static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
+static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>::C % Tune<StepTable>::B == 0,
+              "chunk must be a multiple of the block");
 
 // Per-lane run state. Positions are relative to the lane's chunk start `cs`.
 struct LaneRun {
@@ -221,8 +250,8 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
   s = s3;
 }
 
-template <class Step, int E, bool DIRECT>
-__device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[kBlk / 16], uint64_t pos,
+template <int BK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
   b.pos = pos;
@@ -233,10 +262,10 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   b.lastj = -1;
   uint32_t s = r.s;
   // word j's state-independent work (Step::prep) is issued one word ahead
-  constexpr int NW = kBlk / 4;
+  constexpr int NW = BK / 4;
   uint32_t w[NW];
 #pragma unroll
-  for (int i = 0; i < kBlk / 16; ++i) {
+  for (int i = 0; i < BK / 16; ++i) {
     w[4 * i + 0] = v[i].x;
     w[4 * i + 1] = v[i].y;
     w[4 * i + 2] = v[i].z;
@@ -244,17 +273,15 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   }
   typename Step::Pre pre = st.prep(w[0]);
 #define DG_W(J)                                                                         \
-  {                                                                                     \
+  if ((J) < NW) {                                                                       \
     const typename Step::Pre cur = pre;                                                 \
-    if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : (J)]);                   \
-    word_step<J>(st, M, w[J], cur, s, b, r, emit);                                      \
+    if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : 0]);                     \
+    word_step<J>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit);                     \
   }
   DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
   DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
-#if DGREP_BLOCK == 128
   DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
   DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
-#endif
 #undef DG_W
   r.s = s;
   r.nl = b.nl0 + b.nlrun;
@@ -265,13 +292,14 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   }
 }
 
-__device__ __forceinline__ void load_block(uint4 (&v)[kBlk / 16], const uint8_t* p) {
+template <int BK>
+__device__ __forceinline__ void load_block(uint4 (&v)[BK / 16], const uint8_t* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-  for (int i = 0; i < kBlk / 16; ++i) v[i] = q[i];
+  for (int i = 0; i < BK / 16; ++i) v[i] = q[i];
 }
 
-// The last < 64 bytes of the split, one byte at a time, then the end of the
+// The last < BLOCK bytes of the split, one byte at a time, then the end of the
 // split closes the last owned line (strings.Split's final piece).
 template <class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8_t* p, uint64_t pos, uint64_t avail, uint64_t C,
@@ -293,10 +321,10 @@ __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8
   if (!r.term && r.seen && Step::is(st.byte(r.s, uint32_t('\n')), M)) emit(r, avail, r.prev_nl + 1, r.nl);
 }
 
-// Runs one lane (see file comment) over 64-byte blocks, prefetching the next
+// Runs one lane (see file comment) over BK-byte blocks, prefetching the next
 // block while the current one is stepped (two register buffers, ping-pong).
 // Returns the number of '\n' inside the lane's own chunk [cs, cs + C).
-template <int C, class Step, int E, bool DIRECT>
+template <int C, int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
                                              const Emitter<E, DIRECT>& emit) {
   const uint32_t M = a.start_m;
@@ -312,22 +340,22 @@ __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, 
   uint32_t nl_chunk = 0;
   bool snap = false;
   uint64_t pos = 0;
-  uint4 A[kBlk / 16], B[kBlk / 16];
-  if (avail >= kBlk) load_block(A, p);
+  uint4 A[BK / 16], B[BK / 16];
+  if (avail >= BK) load_block<BK>(A, p);
   for (;;) {
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
-    if (pos + kBlk > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
-    load_block(B, p + (pos + 2 * kBlk <= avail ? pos + kBlk : pos));  // prefetch (or a harmless re-read)
-    run_block(st, M, A, pos, uint64_t(C), r, emit);
-    pos += kBlk;
+    if (pos + BK > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
+    load_block<BK>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
+    run_block<BK>(st, M, A, pos, uint64_t(C), r, emit);
+    pos += BK;
 
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
-    if (pos + kBlk > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
-    load_block(A, p + (pos + 2 * kBlk <= avail ? pos + kBlk : pos));
-    run_block(st, M, B, pos, uint64_t(C), r, emit);
-    pos += kBlk;
+    if (pos + BK > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
+    load_block<BK>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
+    run_block<BK>(st, M, B, pos, uint64_t(C), r, emit);
+    pos += BK;
   }
   if (!snap) nl_chunk = r.nl;
   return nl_chunk;
@@ -346,8 +374,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
 // the tile's exclusive scans run on the wave's lanes (DPP/bpermute) and one
 // lane reserves the tile's staging range with a single atomic.
-template <class Step, int C, int E, int TBL>
+template <class Step, int TBL>
 __global__ __launch_bounds__(kScanThreads) void scan_dfa8_kernel(ScanArgs a) {
+  constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
   __shared__ ScanSmem<TBL, E> sm;
   const int tid = int(threadIdx.x);
   for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += kScanThreads * 16u)
@@ -362,7 +391,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_dfa8_kernel(ScanArgs a) {
     const uint64_t cs = t * uint64_t(kTileLanes) * uint64_t(C) + uint64_t(lane) * uint64_t(C);
     LaneRun r;
     Emitter<E, false> em{&a, slots, cs, 0, 0};
-    const uint32_t nlc = run_lane<C>(a, st, cs, r, em);
+    const uint32_t nlc = run_lane<C, BK>(a, st, cs, r, em);
     const uint32_t nev = r.nev;
 
     // tile-wide exclusive scans of (newlines, matching lines) across the wave
@@ -413,8 +442,9 @@ __global__ __launch_bounds__(kScanThreads) void scan_dfa8_kernel(ScanArgs a) {
 
 // Lanes that owned more matching lines than their LDS slots: one thread per
 // such lane runs it again in direct-write mode (rare: dense short matches).
-template <class Step, int C, int E, int TBL>
+template <class Step, int TBL>
 __global__ __launch_bounds__(64) void scan_overflow_kernel(ScanArgs a, uint64_t nover) {
+  constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
   __shared__ ScanSmem<TBL, 1> sm;
   for (uint32_t i = threadIdx.x * 16u; i < a.table_bytes; i += 64 * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
@@ -424,7 +454,7 @@ __global__ __launch_bounds__(64) void scan_overflow_kernel(ScanArgs a, uint64_t 
     const OverflowLane ol = a.overflow[k];
     LaneRun r;
     Emitter<E, true> ed{&a, nullptr, ol.cs, ol.out_base, ol.nl_prefix};
-    run_lane<C>(a, st, ol.cs, r, ed);
+    run_lane<C, BK>(a, st, ol.cs, r, ed);
   }
 }
 
@@ -532,28 +562,27 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
 
 // ---- host-side launchers (called from dgrep_runtime.cpp) ----------------
 
-constexpr int kChunk = DGREP_CHUNK;  // bytes per lane chunk (multiple of 128)
-constexpr int kSlots = DGREP_SLOTS;  // LDS slots per lane for matching lines
-
-uint64_t scan_tile_bytes() { return uint64_t(kTileLanes) * kChunk; }
+uint64_t scan_tile_bytes(int kind) {
+  return uint64_t(kTileLanes) * uint64_t(kind == kStepSheng8 ? Tune<StepSheng8>::C : Tune<StepTable>::C);
+}
 uint32_t scan_table_row() { return kRow; }
 
 namespace {
 template <class Step, int TBL>
 hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((scan_dfa8_kernel<Step, kChunk, kSlots, TBL>), dim3(grid), dim3(kScanThreads), 0, stream, a);
+  hipLaunchKernelGGL((scan_dfa8_kernel<Step, TBL>), dim3(grid), dim3(kScanThreads), 0, stream, a);
   return hipGetLastError();
 }
 template <class Step, int TBL>
 hipError_t overflow_t(const ScanArgs& a, uint64_t nover, hipStream_t stream) {
   int grid = int((nover + 63) / 64);
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL((scan_overflow_kernel<Step, kChunk, kSlots, TBL>), dim3(grid), dim3(64), 0, stream, a, nover);
+  hipLaunchKernelGGL((scan_overflow_kernel<Step, TBL>), dim3(grid), dim3(64), 0, stream, a, nover);
   return hipGetLastError();
 }
 template <class Step, int TBL>
 hipError_t occ_t(int* b) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, kChunk, kSlots, TBL>, kScanThreads,
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL>, kScanThreads,
                                                       0);
 }
 

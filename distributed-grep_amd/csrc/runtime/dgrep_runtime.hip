@@ -20,7 +20,7 @@
 
 namespace dgrep {
 // scan_dfa.hip
-uint64_t scan_tile_bytes();
+uint64_t scan_tile_bytes(int kind);
 uint32_t scan_table_row();
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu);
 hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
@@ -222,7 +222,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     c->err = "device split must be 16-byte aligned";
     return DGREP_E_INVALID;
   }
-  const uint64_t tile = scan_tile_bytes();
+  const uint64_t tile = scan_tile_bytes(c->step_kind);
   const uint64_t ntiles = (n + tile - 1) / tile;
   int rc;
   if ((rc = grow(c, &c->d_tiles, &c->tiles_cap, ntiles)) != DGREP_OK) return rc;

@@ -81,8 +81,9 @@ def test_random_small(gpu_ctx, pattern):
         _check(gpu_ctx, pattern, data)
 
 
-@pytest.mark.parametrize("size", [1, 63, 64, 1023, 1024, 1025, 2048, 2049, 131071, 131072, 131073, 262143, 262144,
-                                  262145, 3 * 262144 + 17])
+# chunk edges: 1 KiB (table stepper) / 4 KiB (Sheng); tile edges: 64 KiB / 256 KiB
+@pytest.mark.parametrize("size", [1, 63, 64, 127, 128, 129, 1023, 1024, 1025, 2048, 2049, 4095, 4096, 4097, 65535,
+                                  65536, 65537, 131071, 131072, 131073, 262143, 262144, 262145, 3 * 262144 + 17])
 def test_tile_and_chunk_boundaries(gpu_ctx, size):
     import dgrep
 
@@ -92,7 +93,7 @@ def test_tile_and_chunk_boundaries(gpu_ctx, size):
         if edge < size:
             data[edge] = 0x0A
     data = bytes(data)
-    for pattern in (b"error", b"", b"^2024", b"ok$"):
+    for pattern in (b"error", b"", b"^2024", b"ok$", b"(WARN|ERROR) [a-z_]+"):
         _check(gpu_ctx, pattern, data)
 
 
