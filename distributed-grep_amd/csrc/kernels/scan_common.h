@@ -46,6 +46,11 @@ struct ScanArgs {
   OverflowLane* overflow;
   uint64_t overflow_cap;
   unsigned long long* overflow_count;
+  // kStepWide only: the whole [state][class] u16 table in HBM (L2-resident);
+  // its first `hot_entries` entries are also in the LDS image
+  const uint16_t* wide;
+  uint32_t nclasses;
+  uint32_t hot_entries;
 };
 
 enum : uint32_t { kStatusLineTooLong = 1u };
@@ -57,6 +62,15 @@ constexpr int kTileLanes = 64;     // a tile is one wave's 64 chunks
 enum : int {
   kStepTable = 0,   // <= 256 states: u8 [state][byte] table, 260-byte rows
   kStepSheng8 = 1,  // <= 8 states: per-byte 8-state vectors (v_perm stepping)
+  kStepWide = 2,    // <= 65535 states: u16 [state][class] table, hot rows in LDS, all rows in HBM
 };
+
+// LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
+// runtime renumbers states hottest-first (start, start_m, then BFS order from
+// start), so the shallow states an Aho-Corasick-like automaton spends nearly
+// all its steps in are LDS-resident and the deep ones are read from L2.
+constexpr uint32_t kWideClassBytes = 256;
+constexpr uint32_t kWideHotBytes = 96 * 1024;
+constexpr int kWideThreads = 1024;  // one workgroup per CU shares one LDS copy
 
 }  // namespace dgrep

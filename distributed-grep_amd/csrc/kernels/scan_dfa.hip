@@ -66,6 +66,15 @@
 #ifndef DGREP_TABLE_BLOCK
 #define DGREP_TABLE_BLOCK 64
 #endif
+#ifndef DGREP_WIDE_CHUNK
+#define DGREP_WIDE_CHUNK 1024
+#endif
+#ifndef DGREP_WIDE_SLOTS
+#define DGREP_WIDE_SLOTS 4
+#endif
+#ifndef DGREP_WIDE_BLOCK
+#define DGREP_WIDE_BLOCK 64
+#endif
 #ifndef DGREP_SHENG_SCHED_BARRIER
 #define DGREP_SHENG_SCHED_BARRIER 0
 #endif
@@ -86,10 +95,10 @@ __device__ __forceinline__ uint32_t hi_byte(uint32_t m) { return (31u - __clz(m)
 // different states that read the same input byte hit different banks.
 constexpr uint32_t kRow = 260;
 
-template <int TBL, int E>
+template <int TBL, int E, int NT>
 struct ScanSmem {
   alignas(16) uint8_t tbl[TBL];  // first member: the table sits at LDS address 0
-  uint32_t slots[kScanThreads * E * 2];
+  uint32_t slots[NT * E * 2];
 };
 
 // DFA of at most 256 states: u8 transition table, row s at LDS s*260.
@@ -143,13 +152,51 @@ struct StepSheng8 {
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return (s & 0xffu) == M; }
 };
 
+// DFA of at most 65535 states (large alternations, SURVEY config 4): u16
+// next-state table [state][class]. The hot rows (lowest state numbers, see
+// kWideHotBytes) are read from LDS, the rest from HBM through L2; the branch
+// is per lane and almost always wave-uniform. The class lookups depend only on
+// the input word and are issued a word ahead.
+struct StepWide {
+  static constexpr int kKind = kStepWide;
+  const uint8_t* cls;    // LDS: byte -> class
+  const uint16_t* hot;   // LDS: rows 0 .. hot_entries / nc - 1
+  const uint16_t* full;  // HBM: every row
+  uint32_t nc, hot_entries;
+  __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t c) const {
+    const uint32_t i = __umul24(s, nc) + c;
+    if (__builtin_expect(i < hot_entries, 1)) return hot[i];
+    return full[i];
+  }
+  struct Pre {
+    uint32_t c0, c1, c2, c3;
+  };
+  __device__ __forceinline__ Pre prep(uint32_t x) const {
+    return Pre{cls[x & 0xffu], cls[(x >> 8) & 0xffu], cls[(x >> 16) & 0xffu], cls[x >> 24]};
+  }
+  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                        uint32_t& s3) const {
+    s0 = one(s, p.c0);
+    s1 = one(s0, p.c1);
+    s2 = one(s1, p.c2);
+    s3 = one(s2, p.c3);
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return one(s, cls[b]); }
+  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
+};
+
 template <class Step>
-__device__ __forceinline__ Step make_step(const uint8_t* lds);
+__device__ __forceinline__ Step make_step(const uint8_t* lds, const ScanArgs& a);
 template <>
-__device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds) { return StepTable{lds}; }
+__device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }
 template <>
-__device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds) {
+__device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds, const ScanArgs&) {
   return StepSheng8{reinterpret_cast<const uint2*>(lds)};
+}
+template <>
+__device__ __forceinline__ StepWide make_step<StepWide>(const uint8_t* lds, const ScanArgs& a) {
+  return StepWide{lds, reinterpret_cast<const uint16_t*>(lds + kWideClassBytes), a.wide, a.nclasses,
+                  a.hot_entries};
 }
 
 template <class Step>
@@ -161,6 +208,10 @@ struct Tune<StepSheng8> {
 template <>
 struct Tune<StepTable> {
   static constexpr int C = DGREP_TABLE_CHUNK, E = DGREP_TABLE_SLOTS, B = DGREP_TABLE_BLOCK;
+};
+template <>
+struct Tune<StepWide> {
+  static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK;
 };
 static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
@@ -222,7 +273,7 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
   // StepTable: keep each word's work in place (hoisting the chain-independent
   // newline masks of a whole block costs ~100 VGPRs). StepSheng8 wants the
   // opposite: its state-independent LDS reads should run ahead of the chain.
-  if (Step::kKind == kStepTable || DGREP_SHENG_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);
+  if (Step::kKind != kStepSheng8 || DGREP_SHENG_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);
   const uint32_t m = nl_mask(x);
   uint32_t s0, s1, s2, s3;
   st.apply(pre, s, s0, s1, s2, s3);
@@ -374,20 +425,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
 // the tile's exclusive scans run on the wave's lanes (DPP/bpermute) and one
 // lane reserves the tile's staging range with a single atomic.
-template <class Step, int TBL>
-__global__ __launch_bounds__(kScanThreads) void scan_dfa8_kernel(ScanArgs a) {
+template <class Step, int TBL, int NT>
+__global__ __launch_bounds__(NT) void scan_dfa8_kernel(ScanArgs a) {
   constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
-  __shared__ ScanSmem<TBL, E> sm;
+  __shared__ ScanSmem<TBL, E, NT> sm;
   const int tid = int(threadIdx.x);
-  for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += kScanThreads * 16u)
+  for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += NT * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
   __syncthreads();
 
-  const Step st = make_step<Step>(sm.tbl);
+  const Step st = make_step<Step>(sm.tbl, a);
   uint32_t* slots = sm.slots + tid * E * 2;
   const int lane = tid & 63;
-  const uint64_t waves = uint64_t(gridDim.x) * (kScanThreads / 64);
-  for (uint64_t t = uint64_t(blockIdx.x) * (kScanThreads / 64) + uint64_t(tid >> 6); t < a.ntiles; t += waves) {
+  const uint64_t waves = uint64_t(gridDim.x) * (NT / 64);
+  for (uint64_t t = uint64_t(blockIdx.x) * (NT / 64) + uint64_t(tid >> 6); t < a.ntiles; t += waves) {
     const uint64_t cs = t * uint64_t(kTileLanes) * uint64_t(C) + uint64_t(lane) * uint64_t(C);
     LaneRun r;
     Emitter<E, false> em{&a, slots, cs, 0, 0};
@@ -445,11 +496,11 @@ __global__ __launch_bounds__(kScanThreads) void scan_dfa8_kernel(ScanArgs a) {
 template <class Step, int TBL>
 __global__ __launch_bounds__(64) void scan_overflow_kernel(ScanArgs a, uint64_t nover) {
   constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
-  __shared__ ScanSmem<TBL, 1> sm;
+  __shared__ ScanSmem<TBL, 1, 64> sm;
   for (uint32_t i = threadIdx.x * 16u; i < a.table_bytes; i += 64 * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
   __syncthreads();
-  const Step st = make_step<Step>(sm.tbl);
+  const Step st = make_step<Step>(sm.tbl, a);
   for (uint64_t k = uint64_t(blockIdx.x) * 64 + threadIdx.x; k < nover; k += uint64_t(gridDim.x) * 64) {
     const OverflowLane ol = a.overflow[k];
     LaneRun r;
@@ -563,14 +614,18 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
 // ---- host-side launchers (called from dgrep_runtime.cpp) ----------------
 
 uint64_t scan_tile_bytes(int kind) {
-  return uint64_t(kTileLanes) * uint64_t(kind == kStepSheng8 ? Tune<StepSheng8>::C : Tune<StepTable>::C);
+  const int C = kind == kStepSheng8 ? Tune<StepSheng8>::C : kind == kStepWide ? Tune<StepWide>::C : Tune<StepTable>::C;
+  return uint64_t(kTileLanes) * uint64_t(C);
 }
 uint32_t scan_table_row() { return kRow; }
 
 namespace {
+template <class Step>
+constexpr int threads_of() { return Step::kKind == kStepWide ? kWideThreads : kScanThreads; }
 template <class Step, int TBL>
 hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((scan_dfa8_kernel<Step, TBL>), dim3(grid), dim3(kScanThreads), 0, stream, a);
+  constexpr int NT = threads_of<Step>();
+  hipLaunchKernelGGL((scan_dfa8_kernel<Step, TBL, NT>), dim3(grid), dim3(NT), 0, stream, a);
   return hipGetLastError();
 }
 template <class Step, int TBL>
@@ -582,14 +637,15 @@ hipError_t overflow_t(const ScanArgs& a, uint64_t nover, hipStream_t stream) {
 }
 template <class Step, int TBL>
 hipError_t occ_t(int* b) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL>, kScanThreads,
-                                                      0);
+  constexpr int NT = threads_of<Step>();
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL, NT>, NT, 0);
 }
 
 // One switch for every entry point: stepper by kind, LDS image by size.
 template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
+  if (kind == kStepWide) return op.template run<StepWide, int(kWideClassBytes + kWideHotBytes)>();
   if (table_bytes <= 16 * kRow) return op.template run<StepTable, 16 * kRow>();
   if (table_bytes <= 32 * kRow) return op.template run<StepTable, 32 * kRow>();
   if (table_bytes <= 64 * kRow) return op.template run<StepTable, 64 * kRow>();

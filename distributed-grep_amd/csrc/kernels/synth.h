@@ -41,9 +41,11 @@ struct Rng {
   DG_HD uint32_t below(uint32_t n) { return uint32_t((next() >> 32) * uint64_t(n) >> 32); }
 };
 
-// keyword i of `seed` (lowercase a-z, 5..12 letters); returns its length
+// keyword i of `seed` (lowercase a-z, 5..12 letters); returns its length.
+// The set depends on seed % 1000 only, so the splits of a multi-GPU run
+// (seed + 1000 * rank) plant the same keywords.
 DG_HD int keyword(uint64_t seed, int i, char* out) {
-  Rng r{mix(seed ^ 0x6b6579776f726473ull) ^ mix(uint64_t(i) + 0x1234)};
+  Rng r{mix((seed % 1000) ^ 0x6b6579776f726473ull) ^ mix(uint64_t(i) + 0x1234)};
   int len = 5 + int(r.below(8));
   for (int k = 0; k < len; ++k) out[k] = char('a' + r.below(26));
   return len;

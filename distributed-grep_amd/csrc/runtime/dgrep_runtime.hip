@@ -46,6 +46,11 @@ struct dgrep_ctx {
   bool empty_line_matches = false;
   uint8_t* d_table = nullptr;  // stepper image (see dgrep_load_dfa)
   uint32_t table_bytes = 0;
+  uint16_t* d_wide = nullptr;  // kStepWide: the whole u16 [state][class] table
+  uint32_t nclasses = 0, hot_entries = 0;
+  // dgrep_set_stepper: force the wide stepper / cap its LDS rows (tests, tuning)
+  bool force_wide = false;
+  uint32_t wide_hot_rows_cap = UINT32_MAX;
   int step_kind = kStepTable;
   int blocks_per_cu = 1;
 
@@ -125,7 +130,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -140,6 +145,13 @@ extern "C" const char* dgrep_last_error(dgrep_ctx* c) { return c ? c->err.c_str(
 extern "C" int dgrep_set_stream(dgrep_ctx* c, void* s) {
   if (!c) return DGREP_E_INVALID;
   c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_set_stepper(dgrep_ctx* c, int force_wide, uint32_t wide_hot_rows) {
+  if (!c) return DGREP_E_INVALID;
+  c->force_wide = force_wide != 0;
+  c->wide_hot_rows_cap = wide_hot_rows ? wide_hot_rows : UINT32_MAX;
   return DGREP_OK;
 }
 
@@ -159,14 +171,42 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
       c->err = "dgrep_load_dfa: transition out of range";
       return DGREP_E_INVALID;
     }
-  if (h.nstates > 256) {
+  if (h.nstates > 65535) {
     c->err = "dgrep_load_dfa: DFA has " + std::to_string(h.nstates) +
-             " states; this build scans DFAs of at most 256 states (LDS-resident u8 table)";
+             " states; the wide stepper indexes states with u16 (at most 65535)";
     return DGREP_E_UNSUPPORTED;
   }
   // expand byte classes into the kernel's LDS image
   std::vector<uint8_t> t;
-  if (h.nstates <= 8) {
+  std::vector<uint16_t> wide;
+  uint32_t start = h.start, start_m = h.start_m;
+  if (h.nstates > 256 || c->force_wide) {
+    // StepWide: renumber hottest-first -- start, start_m, then breadth-first
+    // from start -- so the shallow states sit in the LDS-resident rows
+    c->step_kind = kStepWide;
+    const uint32_t S = h.nstates, K = h.nclasses;
+    std::vector<uint32_t> order, id(S, UINT32_MAX);
+    order.reserve(S);
+    auto visit = [&](uint32_t x) {
+      if (id[x] == UINT32_MAX) { id[x] = uint32_t(order.size()); order.push_back(x); }
+    };
+    visit(h.start);
+    visit(h.start_m);
+    for (size_t q = 0; q < order.size(); ++q)
+      for (uint32_t k = 0; k < K; ++k) visit(trans[size_t(order[q]) * K + k]);
+    for (uint32_t x = 0; x < S; ++x) visit(x);  // unreachable states (none in a minimal DFA)
+    wide.resize(size_t(S) * K);
+    for (uint32_t n = 0; n < S; ++n)
+      for (uint32_t k = 0; k < K; ++k) wide[size_t(n) * K + k] = uint16_t(id[trans[size_t(order[n]) * K + k]]);
+    start = id[h.start];
+    start_m = id[h.start_m];
+    const uint32_t hot_rows = std::min<uint32_t>({S, kWideHotBytes / (2 * K), c->wide_hot_rows_cap});
+    c->hot_entries = hot_rows * K;
+    c->nclasses = K;
+    t.assign((kWideClassBytes + size_t(c->hot_entries) * 2 + 15) & ~size_t(15), 0);
+    memcpy(t.data(), h.byte_class, 256);
+    memcpy(t.data() + kWideClassBytes, wide.data(), size_t(c->hot_entries) * 2);
+  } else if (h.nstates <= 8) {
     // StepSheng8: V[b] = 8 bytes, byte s = next state of s on input byte b
     c->step_kind = kStepSheng8;
     t.assign(256 * 8, 0);
@@ -183,13 +223,19 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   }
   if (c->d_table) HIPCHK(hipFree(c->d_table));
   c->d_table = nullptr;
+  if (c->d_wide) HIPCHK(hipFree(c->d_wide));
+  c->d_wide = nullptr;
   c->table_bytes = uint32_t(t.size());
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_table), (t.size() + 15) & ~size_t(15)));
   HIPCHK(hipMemcpy(c->d_table, t.data(), t.size(), hipMemcpyHostToDevice));
+  if (!wide.empty()) {
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_wide), wide.size() * 2));
+    HIPCHK(hipMemcpy(c->d_wide, wide.data(), wide.size() * 2, hipMemcpyHostToDevice));
+  }
   c->flags = h.flags;
   c->nstates = h.nstates;
-  c->start = h.start;
-  c->start_m = h.start_m;
+  c->start = start;
+  c->start_m = start_m;
   c->empty_line_matches = trans[size_t(h.start) * h.nclasses + h.byte_class[uint8_t('\n')]] == h.start_m;
   int bpc = 0;
   HIPCHK(scan_dfa_occupancy(c->step_kind, c->table_bytes, &bpc));
@@ -248,6 +294,9 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.tiles = c->d_tiles;
   a.status = reinterpret_cast<uint32_t*>(c->d_counters + 2);
   a.overflow_count = c->d_counters + 1;
+  a.wide = c->d_wide;
+  a.nclasses = c->nclasses;
+  a.hot_entries = c->hot_entries;
   const uint64_t resident = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
   const int grid = int(std::min<uint64_t>(ntiles, resident));
   unsigned long long ctr[4] = {0, 0, 0, 0};

@@ -51,7 +51,7 @@ EXPORTS = (
     "dgrep_compile", "dgrep_blob_free", "dgrep_blob_info_get", "dgrep_open", "dgrep_close",
     "dgrep_last_error", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
-    "dgrep_last_kernel_ms",
+    "dgrep_last_kernel_ms", "dgrep_set_stepper",
 )
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
@@ -106,6 +106,8 @@ def lib() -> ctypes.CDLL:
             L.dgrep_set_stream.restype = i
             L.dgrep_load_dfa.argtypes = [vp, vp, sz]
             L.dgrep_load_dfa.restype = i
+            L.dgrep_set_stepper.argtypes = [vp, i, ctypes.c_uint32]
+            L.dgrep_set_stepper.restype = i
             L.dgrep_scan.argtypes = [vp, vp, sz, ctypes.POINTER(_Result)]
             L.dgrep_scan.restype = i
             L.dgrep_result_free.argtypes = [ctypes.POINTER(_Result)]
@@ -203,6 +205,11 @@ class Context:
 
     def set_stream(self, hip_stream: int):
         self._check(self._L.dgrep_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
+    def set_stepper(self, force_wide: bool = False, wide_hot_rows: int = 0):
+        """Testing/tuning: force the wide stepper and/or cap its LDS rows for
+        the next load() (dgrep_set_stepper)."""
+        self._check(self._L.dgrep_set_stepper(self._h, int(force_wide), wide_hot_rows))
 
     def load(self, pattern) -> CompiledPattern:
         cp = pattern if isinstance(pattern, CompiledPattern) else CompiledPattern(pattern)

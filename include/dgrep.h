@@ -91,6 +91,11 @@ const char* dgrep_last_error(dgrep_ctx* ctx);
  * NULL selects the context's own stream. */
 int dgrep_set_stream(dgrep_ctx* ctx, void* hip_stream);
 int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
+/* Stepper selection for later dgrep_load_dfa calls (tests / tuning only; the
+ * default picks by state count: <= 8 Sheng, <= 256 u8 table, else wide).
+ * force_wide != 0 uses the wide (u16, LDS-hot + HBM) stepper for any DFA;
+ * wide_hot_rows != 0 caps its LDS-resident rows. */
+int dgrep_set_stepper(dgrep_ctx* ctx, int force_wide, uint32_t wide_hot_rows);
 
 /* Host bytes -> H2D -> scan -> D2H results. This is the call Map makes. */
 int dgrep_scan(dgrep_ctx* ctx, const uint8_t* data, size_t n, dgrep_result* out);

@@ -40,7 +40,12 @@ def _oracle(pattern, data, threads=1):
 
 
 def _check(ctx, pattern, data, threads=1):
-    ctx.load(pattern)
+    import dgrep
+
+    if isinstance(pattern, dgrep.CompiledPattern):
+        pattern = pattern.pattern
+    else:
+        ctx.load(pattern)
     ln, st, le = ctx.scan(data)
     oln, ost, ole = _oracle(pattern, data, threads)
     assert len(ln) == len(oln), (pattern, len(ln), len(oln))
@@ -169,3 +174,51 @@ def test_map_reduce_surface(gpu_ctx):
     assert len(dgrep.Map("f", "a\nb\n")) == 3  # trailing empty line matches ""
     dgrep.set_pattern("a**")
     assert dgrep.Map("f", "a\n") == []
+
+
+# ---- the wide stepper (u16 table, hot rows in LDS, the rest in HBM) ---------
+@pytest.fixture
+def wide_ctx(gpu_ctx):
+    yield gpu_ctx
+    gpu_ctx.set_stepper(False, 0)
+
+
+@pytest.mark.parametrize("hot_rows", [0, 2])  # 0: as many LDS rows as fit; 2: nearly every row from HBM
+@pytest.mark.parametrize("pattern", PATTERNS)
+def test_wide_stepper_forced(wide_ctx, pattern, hot_rows):
+    wide_ctx.set_stepper(True, hot_rows)
+    rnd = random.Random(hash(pattern) & 0xfff)
+    alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\xe2\x82\xac", b"\xff",
+             b"WARN", b"ERROR", b"error", b"2024-01", b"key "]
+    for n in (0, 1, 100, 5000, 70000, 300000):
+        data = b"".join(rnd.choice(alpha) for _ in range(n // 3))
+        _check(wide_ctx, pattern, data)
+
+
+def test_wide_stepper_boundaries_and_overflow(wide_ctx):
+    import dgrep
+
+    wide_ctx.set_stepper(True, 3)
+    for size in (1023, 1024, 1025, 65535, 65536, 65537, 3 * 65536 + 17):
+        data = bytearray(dgrep.synth_corpus_host(size, 11, 0))
+        for edge in (1023, 1024, 65535, 65536):
+            if edge < size:
+                data[edge] = 0x0A
+        for pattern in (b"error", b"", b"^2024", b"(WARN|ERROR) [a-z_]+"):
+            _check(wide_ctx, pattern, bytes(data))
+    data = b"\n".join(b"error %d" % i for i in range(100000))
+    _check(wide_ctx, b"error", data)
+
+
+@pytest.mark.parametrize("nkw,size", [(200, 4 << 20), (1000, 1 << 20)])
+def test_keyword_alternation_c4(gpu_ctx, nkw, size):
+    """SURVEY config 4: (?i) alternation of seeded keywords (> 256 DFA states)."""
+    import dgrep
+
+    kws = dgrep.synth_keywords(4, nkw)
+    pattern = b"(?i)(" + b"|".join(kws) + b")"
+    cp = gpu_ctx.load(pattern)
+    assert cp.nstates > 256
+    data = dgrep.synth_corpus_host(size, 4, 1)
+    n = _check(gpu_ctx, cp, data, threads=16)
+    assert n > 0
