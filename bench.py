@@ -37,7 +37,7 @@ WORKLOADS = {
                 desc="C2 (long planted literal): 16 GiB split (seed 2)"),
     "c3": dict(pattern="^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", seed=3, kind=0, gib=16.0,
                desc="C3: 16 GiB split (seed 3), anchored regex with classes/alternation"),
-    "c4": dict(pattern=None, seed=4, kind=1, gib=16.0,
+    "c4": dict(pattern=None, seed=4, kind=1, gib=16.0, verify_window=256 << 10,
                desc="C4: 16 GiB split (seed 4, keywords planted), (?i) alternation of 1,000 seeded keywords, "
                     "wide DFA (hot rows in LDS, the rest in HBM/L2)"),
 }
@@ -154,7 +154,7 @@ def main():
     verified = None
     if rank == 0 and args.verify_windows > 0:
         verified = verify_windows(buf, n, line_t[:count], start_t[:count], len_t[:count], pattern,
-                                  args.verify_windows)
+                                  args.verify_windows, wl.get("verify_window", 2 << 20))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -216,7 +216,7 @@ def main():
         dist.destroy_process_group()
 
 
-def verify_windows(buf, n, line_t, start_t, len_t, pattern, k):
+def verify_windows(buf, n, line_t, start_t, len_t, pattern, k, win):
     """Parity at full size: random whole-line windows of the split re-run on the
     oracle (lines renumbered by the '\\n' count before the window, counted on the
     GPU) must equal the GPU records inside the window; records must be strictly
@@ -230,7 +230,6 @@ def verify_windows(buf, n, line_t, start_t, len_t, pattern, k):
     if line_t.numel() > 1:
         assert bool((line_t[1:] > line_t[:-1]).all()), "line numbers not strictly ascending"
     rng = np.random.default_rng(12345)
-    win = 2 << 20
     ok = 0
     for _ in range(k):
         a0 = int(rng.integers(0, max(1, n - win)))
@@ -242,7 +241,7 @@ def verify_windows(buf, n, line_t, start_t, len_t, pattern, k):
         a, b = a0 + i + 1, a0 + j  # whole lines [a, b), b = a '\n'
         text = chunk[i + 1:j]
         nl_before = int((buf[:a] == 10).sum().item())
-        oln, ost, ole = O.grep_map(pattern.encode(), text)
+        oln, ost, ole = O.grep_map(pattern.encode(), text, threads=min(16, os.cpu_count() or 1))
         sel = (start_t >= a) & (start_t < b)
         gl = line_t[sel].cpu().numpy().astype(np.int64)
         gs = start_t[sel].cpu().numpy().astype(np.int64)
@@ -251,6 +250,7 @@ def verify_windows(buf, n, line_t, start_t, len_t, pattern, k):
         np.testing.assert_array_equal(gs, ost.astype(np.int64) + a)
         np.testing.assert_array_equal(ge, ole.astype(np.int64))
         ok += 1
+        log("verified window %d/%d at byte %d (%d matching lines)" % (ok, k, a, len(oln)))
     return ok
 
 

@@ -41,13 +41,15 @@
 #include "scan_common.h"
 
 // build-time tuning knobs, per stepper (defaults are the shipped
-// configuration, chosen by tools/variant_bench.sh on MI355X):
-//   CHUNK  bytes per lane chunk (multiple of BLOCK)
-//   SLOTS  LDS slots per lane for matching lines
-//   BLOCK  bytes per lane per register load block (64 or 128)
-// The Sheng stepper's chain is VALU-only, so it likes long chunks and big
-// blocks; the table stepper's chain waits on LDS and its 2-6 waves/SIMD need
-// the VGPRs a 128-byte block would take.
+// configuration, chosen by tools/variant_bench.sh on MI355X, see DESIGN.md):
+//   CHUNK    bytes per lane chunk (multiple of BLOCK)
+//   SLOTS    LDS slots per lane for matching lines
+//   BLOCK    bytes per lane per register load block (64 or 128)
+//   STAGING  1: full tiles are fetched coalesced through LDS (global_load_lds)
+//   WAVES    waves per SIMD the register allocation must allow
+// Sheng (C2, 7 states): direct per-lane loads, 4 KiB chunks, 128-B blocks:
+// 4.16-4.22 TB/s; the staged variant measured 3.5-3.8 TB/s at 1-2 KiB chunks.
+// Table (C3, 20 states): staged, 2 KiB chunks: 2.83 TB/s (direct 2.67).
 #ifndef DGREP_SHENG_CHUNK
 #define DGREP_SHENG_CHUNK 4096
 #endif
@@ -57,11 +59,27 @@
 #ifndef DGREP_SHENG_BLOCK
 #define DGREP_SHENG_BLOCK 128
 #endif
+#ifndef DGREP_SHENG_STAGING
+#define DGREP_SHENG_STAGING 0
+#endif
 #ifndef DGREP_TABLE_CHUNK
-#define DGREP_TABLE_CHUNK 1024
+#define DGREP_TABLE_CHUNK 2048
 #endif
 #ifndef DGREP_TABLE_SLOTS
-#define DGREP_TABLE_SLOTS 8
+#define DGREP_TABLE_SLOTS 6
+#endif
+#ifndef DGREP_TABLE_STAGING
+#define DGREP_TABLE_STAGING 1
+#endif
+#ifndef DGREP_SHENG_WAVES
+#define DGREP_SHENG_WAVES 3
+#endif
+#ifndef DGREP_TABLE_WAVES
+#define DGREP_TABLE_WAVES 3
+#endif
+// bytes per lane per staged round (global_load_lds path); 128 = whole lines
+#ifndef DGREP_STAGE_ROUND
+#define DGREP_STAGE_ROUND 128
 #endif
 #ifndef DGREP_TABLE_BLOCK
 #define DGREP_TABLE_BLOCK 64
@@ -150,6 +168,21 @@ struct StepSheng8 {
   }
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[b], s); }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return (s & 0xffu) == M; }
+  // map <- transitions of bytes 0..lim of the word applied to the 8-state map
+  // (lo: states 0-3, hi: states 4-7); one v_perm per byte and half
+  __device__ __forceinline__ void compose(const Pre& p, uint32_t lim, uint32_t& lo, uint32_t& hi) const {
+    lo = sel(p.m0, lo);
+    hi = sel(p.m0, hi);
+    const uint32_t l1 = sel(p.m1, lo), h1 = sel(p.m1, hi);
+    lo = lim >= 1 ? l1 : lo;
+    hi = lim >= 1 ? h1 : hi;
+    const uint32_t l2 = sel(p.m2, lo), h2 = sel(p.m2, hi);
+    lo = lim >= 2 ? l2 : lo;
+    hi = lim >= 2 ? h2 : hi;
+    const uint32_t l3 = sel(p.m3, lo), h3 = sel(p.m3, hi);
+    lo = lim >= 3 ? l3 : lo;
+    hi = lim >= 3 ? h3 : hi;
+  }
 };
 
 // DFA of at most 65535 states (large alternations, SURVEY config 4): u16
@@ -166,7 +199,8 @@ struct StepWide {
   __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t c) const {
     const uint32_t i = __umul24(s, nc) + c;
     if (__builtin_expect(i < hot_entries, 1)) return hot[i];
-    return full[i];
+    // global_load_ushort (a generic pointer would compile to flat_load)
+    return ((const __attribute__((address_space(1))) uint16_t*)full)[i];
   }
   struct Pre {
     uint32_t c0, c1, c2, c3;
@@ -226,6 +260,12 @@ struct LaneRun {
   bool seen;         // a line boundary has been crossed (owned lines begin)
   bool term;         // the terminating '\n' at or after the chunk end was consumed
   uint32_t nev;      // matching lines emitted
+  // Sheng staged path: transition map (byte s = state reached from state s) of
+  // the chunk's bytes up to and including its first '\n', and that '\n''s
+  // position (-1: not seen yet). The left neighbour lane finishes its last
+  // owned line with it instead of reading this chunk again.
+  uint32_t mlo, mhi;
+  int32_t p1;
 };
 
 template <int E, bool DIRECT>
@@ -267,7 +307,7 @@ struct Blk {
   int lastj;        // its index
 };
 
-template <int J, class Step, int E, bool DIRECT>
+template <int J, bool TRACK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x, const typename Step::Pre& pre,
                                           uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   // StepTable: keep each word's work in place (hoisting the chain-independent
@@ -296,12 +336,20 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
       emit(r, q0 + k, start, b.nl0 + b.nlrun + uint32_t(__popc(below)));
     }
   }
+  if constexpr (TRACK) {
+    if (r.p1 < 0) {
+      // the chunk's first line piece: compose its transition map (LaneRun::mlo)
+      const uint32_t lim = m ? uint32_t(__builtin_ctz(m)) >> 3 : 3u;
+      st.compose(pre, lim, r.mlo, r.mhi);
+      if (m) r.p1 = int32_t(b.pos + 4u * J + lim);
+    }
+  }
   b.nlrun += uint32_t(__popc(m));
   if (m) { b.lastm = m; b.lastj = J; }
   s = s3;
 }
 
-template <int BK, class Step, int E, bool DIRECT>
+template <int BK, bool TRACK = false, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
@@ -327,7 +375,7 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   if ((J) < NW) {                                                                       \
     const typename Step::Pre cur = pre;                                                 \
     if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : 0]);                     \
-    word_step<J>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit);                     \
+    word_step<J, TRACK>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit);              \
   }
   DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
   DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
@@ -372,27 +420,38 @@ __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8
   if (!r.term && r.seen && Step::is(st.byte(r.s, uint32_t('\n')), M)) emit(r, avail, r.prev_nl + 1, r.nl);
 }
 
-// Runs one lane (see file comment) over BK-byte blocks, prefetching the next
-// block while the current one is stepped (two register buffers, ping-pong).
-// Returns the number of '\n' inside the lane's own chunk [cs, cs + C).
-template <int C, int BK, class Step, int E, bool DIRECT>
-__device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
-                                             const Emitter<E, DIRECT>& emit) {
-  const uint32_t M = a.start_m;
-  const uint64_t avail = cs < a.n ? a.n - cs : 0;
+__device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRun& r) {
   r.s = a.start;
   r.nl = 0;
   r.prev_nl = -1;
   r.seen = (cs == 0);
   r.term = false;
   r.nev = 0;
-  if (avail == 0) return 0;
+  r.mlo = 0x03020100u;  // identity map
+  r.mhi = 0x07060504u;
+  r.p1 = -1;
+}
+
+// Runs a lane (see file comment) from chunk-relative position pos0 over
+// BK-byte blocks with direct per-lane loads, prefetching the next block while
+// the current one is stepped (two register buffers, ping-pong). Returns the
+// number of '\n' inside the lane's own chunk [cs, cs + C).
+template <int C, int BK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step& st, uint64_t cs, uint64_t pos0,
+                                                  LaneRun& r, const Emitter<E, DIRECT>& emit) {
+  const uint32_t M = a.start_m;
+  const uint64_t avail = cs < a.n ? a.n - cs : 0;
+  if (avail <= pos0) {
+    // the split ends exactly here: strings.Split's final piece
+    if (!r.term && r.seen && Step::is(st.byte(r.s, uint32_t('\n')), M)) emit(r, avail, r.prev_nl + 1, r.nl);
+    return r.nl;
+  }
   const uint8_t* __restrict__ p = a.data + cs;
   uint32_t nl_chunk = 0;
   bool snap = false;
-  uint64_t pos = 0;
+  uint64_t pos = pos0;
   uint4 A[BK / 16], B[BK / 16];
-  if (avail >= BK) load_block<BK>(A, p);
+  if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
   for (;;) {
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
@@ -412,6 +471,90 @@ __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, 
   return nl_chunk;
 }
 
+template <int C, int BK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
+                                             const Emitter<E, DIRECT>& emit) {
+  lane_init(a, cs, r);
+  if (cs >= a.n) return 0;
+  return run_lane_from<C, BK>(a, st, cs, 0, r, emit);
+}
+
+// 16 bytes global -> LDS (global_load_lds_dwordx4); the LDS destination is
+// the wave-uniform `lds` + lane * 16. (The builtin exists only in the device
+// compilation pass; the host pass never executes device code.)
+__device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0);
+#endif
+}
+
+// Coalesced variant for a tile lying wholly inside the split. Per round the
+// wave fetches the next R bytes of all 64 lane chunks with
+// global_load_lds_dwordx4: instruction k brings the R-byte segments of lanes
+// k*SPI .. k*SPI+SPI-1 (whole 128-B lines) into LDS row k, the P = R/16 pieces
+// of segment q XOR-rotated by f(q) = (q / (16/P)) % P, which makes every
+// lane's ds_read_b128 of its piece j bank-conflict-free. One ring per wave:
+// the next round is issued as soon as the lane holds its pieces. After the
+// chunk, the lane finishes its last owned line with direct loads.
+template <int C, int R, class Step, int E>
+__device__ __forceinline__ uint32_t run_lane_staged(const ScanArgs& a, const Step& st, uint64_t cs, int lane,
+                                                    uint8_t* stage, LaneRun& r, const Emitter<E, false>& emit) {
+  constexpr int P = R / 16, SPI = 64 / P, G = 16 / P, NR = C / R;
+  static_assert(P * SPI == 64 && C % R == 0, "bad staging shape");
+  lane_init(a, cs, r);
+  const uint32_t M = a.start_m;
+  const uint8_t* tb = a.data + (cs - uint64_t(lane) * uint64_t(C));
+  uint32_t off[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const uint32_t q = uint32_t(k * SPI + lane / P);
+    off[k] = q * uint32_t(C) + 16u * (uint32_t(lane % P) ^ ((q / G) % P));
+  }
+  const uint8_t* rd = stage + (lane / SPI) * 1024 + 16 * ((lane % SPI) * P);
+  const int fl = (lane / G) % P;
+  constexpr bool kTrack = Step::kKind == kStepSheng8;
+#pragma unroll
+  for (int k = 0; k < P; ++k) glds16(tb + off[k], stage + k * 1024);
+  for (int rr = 0; rr < NR; ++rr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint4 v[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) v[j] = *reinterpret_cast<const uint4*>(rd + 16 * (j ^ fl));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (rr + 1 < NR) {
+#pragma unroll
+      for (int k = 0; k < P; ++k)
+        glds16(tb + off[k] + uint32_t(rr + 1) * uint32_t(R), stage + k * 1024);
+    }
+    run_block<R, kTrack>(st, M, v, uint64_t(rr) * R, uint64_t(C), r, emit);
+  }
+  const uint32_t nl_chunk = r.nl;
+  bool tail = true;
+  if constexpr (kTrack) {
+    // The last owned line ends at the right neighbour chunk's first '\n': the
+    // neighbour lane's transition map of that piece finishes it, so the chunk
+    // is not read again. (Lane 63's neighbour belongs to the next tile, and a
+    // neighbour chunk without '\n' means a longer line: those read on.)
+    const uint32_t nlo = __shfl_down(r.mlo, 1, 64), nhi = __shfl_down(r.mhi, 1, 64);
+    const int32_t np1 = __shfl_down(r.p1, 1, 64);
+    if (lane < 63 && np1 >= 0) {
+      tail = false;
+      if (r.seen && (__builtin_amdgcn_perm(nhi, nlo, r.s) & 0xffu) == M)
+        emit(r, uint64_t(C) + uint64_t(np1), r.prev_nl + 1, r.nl);
+    }
+  }
+  if (tail) run_lane_from<C, 64>(a, st, cs, uint64_t(C), r, emit);
+  return nl_chunk;
+}
+
+// the coalesced staged path: small tables only (the staging ring and the
+// table share the CU's LDS)
+template <class Step, int TBL>
+constexpr bool use_staging() {
+  return (DGREP_SHENG_STAGING && Step::kKind == kStepSheng8) ||
+         (DGREP_TABLE_STAGING && Step::kKind == kStepTable && TBL <= 32 * int(kRow));
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = int(threadIdx.x & 63);
 #pragma unroll
@@ -422,13 +565,26 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// waves per SIMD the register allocation must leave room for
+template <class Step>
+constexpr int waves_per_simd() {
+  return Step::kKind == kStepSheng8 ? DGREP_SHENG_WAVES : Step::kKind == kStepTable ? DGREP_TABLE_WAVES : 4;
+}
+
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
 // the tile's exclusive scans run on the wave's lanes (DPP/bpermute) and one
 // lane reserves the tile's staging range with a single atomic.
+
 template <class Step, int TBL, int NT>
-__global__ __launch_bounds__(NT) void scan_dfa8_kernel(ScanArgs a) {
+__global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(ScanArgs a) {
   constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
+  constexpr bool kStaged = use_staging<Step, TBL>();
+  constexpr int R = DGREP_STAGE_ROUND;
   __shared__ ScanSmem<TBL, E, NT> sm;
+  // the staging rings are a __shared__ object of their own: with the table in
+  // the same object, hipcc cannot tell a ring write (global_load_lds) from a
+  // table read and drains vmcnt before every table lookup
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kStaged ? (NT / 64) * 64 * R : 16];
   const int tid = int(threadIdx.x);
   for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += NT * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
@@ -442,7 +598,16 @@ __global__ __launch_bounds__(NT) void scan_dfa8_kernel(ScanArgs a) {
     const uint64_t cs = t * uint64_t(kTileLanes) * uint64_t(C) + uint64_t(lane) * uint64_t(C);
     LaneRun r;
     Emitter<E, false> em{&a, slots, cs, 0, 0};
-    const uint32_t nlc = run_lane<C, BK>(a, st, cs, r, em);
+    uint32_t nlc;
+    if constexpr (kStaged) {
+      // wave-uniform: the whole tile lies inside the split
+      if ((t + 1) * uint64_t(kTileLanes) * uint64_t(C) <= a.n)
+        nlc = run_lane_staged<C, R>(a, st, cs, lane, stage + (tid >> 6) * (64 * R), r, em);
+      else
+        nlc = run_lane<C, BK>(a, st, cs, r, em);
+    } else {
+      nlc = run_lane<C, BK>(a, st, cs, r, em);
+    }
     const uint32_t nev = r.nev;
 
     // tile-wide exclusive scans of (newlines, matching lines) across the wave

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Copy a tools/profile_gpu.sh run into profiles/ (tracked) and update
+profiles/traffic.json, which bench.py reads for roofline.traffic.
+
+    tools/collect_profile.py <gpurun_out/prof_TAG> <round> <workload>
+
+HBM traffic per launch of the scan kernel follows MI355X_MICROARCH.md §HBM:
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half of
+the bytes of wide coalesced streaming reads, so it is doubled; WRITE_SIZE is
+taken as is. Each counter comes from its own --pmc pass.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+
+src, rnd, wl = sys.argv[1], sys.argv[2], sys.argv[3]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+dst = os.path.join(ROOT, "profiles", rnd, wl)
+os.makedirs(dst, exist_ok=True)
+KERNEL = "scan_dfa8_kernel"
+
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+bench = json.load(open(os.path.join(src, "bench_trace.json")))
+json.dump(bench, open(os.path.join(dst, "bench_under_rocprof.json"), "w"), indent=1)
+
+pmc = {}
+for f in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        if KERNEL in r["Kernel_Name"]:
+            pmc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+avg = {k: statistics.mean(v) for k, v in pmc.items()}
+stats = {}
+for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))):
+    if KERNEL in r["Name"]:
+        stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "name": r["Name"]}
+fetch = avg.get("FETCH_SIZE", 0.0) * 1024 * 2
+write = avg.get("WRITE_SIZE", 0.0) * 1024
+n = bench["config"]["split_bytes_per_gpu"]
+summary = {
+    "workload": wl,
+    "kernel": stats,
+    "pmc_avg_per_launch": avg,
+    "hbm_read_bytes_per_launch": fetch,
+    "hbm_write_bytes_per_launch": write,
+    "hbm_bytes_per_launch": fetch + write,
+    "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
+    "traffic_over_algorithmic": (fetch + write) / bench["roofline"]["algorithmic_bytes_per_launch"],
+    "achieved_gbs_rocprof_avg": bench["roofline"]["algorithmic_bytes_per_launch"] / stats["avg_ns"] if stats else None,
+    "bench_hip_event_kernel_ms": bench["roofline"]["kernel_ms_avg"],
+    "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 streaming-read half count), WRITE_SIZE KiB x1024",
+}
+json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+tp = os.path.join(ROOT, "profiles", "traffic.json")
+tr = json.load(open(tp)) if os.path.exists(tp) else {}
+tr[wl] = {"split_bytes": n, "hbm_bytes_per_launch": round(fetch + write), "source": os.path.relpath(dst, ROOT)}
+json.dump(tr, open(tp, "w"), indent=1)
+print(json.dumps(summary, indent=1))

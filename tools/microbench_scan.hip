@@ -263,6 +263,76 @@ __global__ __launch_bounds__(kT) void sheng_multi(const uint8_t* __restrict__ da
   out[2 + blockIdx.x * kT + threadIdx.x] = z;
 }
 
+// V7/V8: coalesced loads through LDS. Per wave and per round, the 64 lanes'
+// next R-byte segments (one per lane chunk, stride C) are fetched with
+// global_load_lds_dwordx4: instruction k brings 64/P whole segments (P = R/16
+// pieces each, so every instruction reads whole 64/128-B lines) into LDS row
+// k; the piece order inside a segment is XOR-rotated by f(q) = (q / (16/P)) % P
+// so the per-lane ds_read_b128 of piece j is bank-conflict-free. Single
+// buffer: the next round is issued as soon as the lane has its pieces in
+// registers.
+template <int R, int MODE>
+__global__ __launch_bounds__(kT) void glds_kernel(const uint8_t* __restrict__ data, uint64_t n, int C,
+                                                  const uint2* vtab, uint32_t* out, uint32_t M) {
+  constexpr int P = R / 16, SPI = 64 / P;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kT / 64][64 * R];
+  __shared__ uint2 V[256];
+  for (int i = threadIdx.x; i < 256; i += kT) V[i] = vtab[i];
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint8_t* st = stage[wv];
+  const uint64_t ntiles = n / (64ull * C);
+  const uint64_t waves = uint64_t(gridDim.x) * (kT / 64);
+  uint32_t acc = 0, s = 0;
+  const int lq = lane / P, lp = lane % P;
+  const int fl = (lane / (16 / P)) % P;
+  for (uint64_t t = uint64_t(blockIdx.x) * (kT / 64) + wv; t < ntiles; t += waves) {
+    const uint8_t* tb = data + t * 64ull * C;
+    auto issue = [&](int r) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const int q = k * SPI + lq;
+        const int pc = lp ^ ((q / (16 / P)) % P);
+        __builtin_amdgcn_global_load_lds((const void*)(tb + uint64_t(q) * C + uint64_t(r) * R + 16 * pc),
+                                         (void*)(st + k * 1024), 16, 0, 0);
+      }
+    };
+    issue(0);
+    const int nr = C / R;
+    for (int r = 0; r < nr; ++r) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint4 v[P];
+#pragma unroll
+      for (int j = 0; j < P; ++j)
+        v[j] = *reinterpret_cast<const uint4*>(st + (lane / SPI) * 1024 + 16 * ((lane % SPI) * P + (j ^ fl)));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (r + 1 < nr) issue(r + 1);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t x = w4[q];
+          if (MODE == 0) {
+            acc ^= x;
+            continue;
+          }
+          const uint2 m0 = V[x & 0xff], m1 = V[(x >> 8) & 0xff], m2 = V[(x >> 16) & 0xff], m3 = V[x >> 24];
+          const uint32_t s0 = __builtin_amdgcn_perm(m0.y, m0.x, s);
+          const uint32_t s1 = __builtin_amdgcn_perm(m1.y, m1.x, s0);
+          const uint32_t s2 = __builtin_amdgcn_perm(m2.y, m2.x, s1);
+          const uint32_t s3 = __builtin_amdgcn_perm(m3.y, m3.x, s2);
+          acc += __popc(nl_mask(x));
+          if (__builtin_expect(((s0 & 0xff) == M) | ((s1 & 0xff) == M) | ((s2 & 0xff) == M) | ((s3 & 0xff) == M), 0))
+            atomicAdd(out + 1, 1u);
+          s = s3;
+        }
+      }
+    }
+  }
+  out[2 + blockIdx.x * kT + threadIdx.x] = acc ^ s;
+}
+
 __global__ void coalesced_kernel(const uint4* __restrict__ d, uint64_t n16, uint32_t* out) {
   uint32_t acc = 0;
   for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x) {
@@ -334,6 +404,24 @@ int main(int argc, char** argv) {
   const uint32_t M = 6;
   auto gbs = [&](float ms) { return double(n) / (ms * 1e-3) / 1e9; };
   const int reps = 5;
+  if (argc > 3) {
+    // glds variants: grid = resident blocks (grid-stride loops must not queue blocks)
+    auto run = [&](const char* name, auto kern) {
+      int occ = 0;
+      CHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kT, 0));
+      const int grid = cus * occ;
+      float ms = timeit([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(kT), 0, 0, d, n, C, vtab, out, M); }, reps);
+      printf("%-22s %d WG/CU %8.1f GB/s\n", name, occ, gbs(ms));
+    };
+    float ms = timeit([&] { coalesced_kernel<<<cus * 8, kT>>>(reinterpret_cast<const uint4*>(d), n / 16, out); }, reps);
+    printf("V0c coalesced          %8.1f GB/s\n", gbs(ms));
+    run("V5b sheng8+nl+event", sheng_kernel<3>);
+    run("V7  glds R=64 xor", glds_kernel<64, 0>);
+    run("V7b glds R=128 xor", glds_kernel<128, 0>);
+    run("V8  glds R=64 sheng", glds_kernel<64, 1>);
+    run("V8b glds R=128 sheng", glds_kernel<128, 1>);
+    return 0;
+  }
   for (int occ : {4, 6, 8}) {
     const int grid = cus * occ;
     printf("--- grid %d WGs (%d per CU), C=%d, n=%.1f GiB\n", grid, occ, C, n / double(1 << 30));

@@ -4,7 +4,7 @@
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 WL=${1:-c2}; shift || true
-VARS=${@:-base sc2k sb64 tc2k tb128}
+VARS=${@:-base sw3 sc2k sr64 tw4}
 for v in $VARS; do
   for rep in 1 2; do
     out=$(DGREP_LIB=$R/distributed-grep_amd/variants/libdgrep_$v.so timeout -k 10 180 python3 $R/bench.py --workload $WL --steps 6 --warmup 2 --no-cpu-baseline --verify-windows 1 2>/dev/null) || { echo "$v FAILED"; exit 1; }
