@@ -71,11 +71,25 @@
 #ifndef DGREP_TABLE_STAGING
 #define DGREP_TABLE_STAGING 1
 #endif
+#ifndef DGREP_SHENG_STREAMS
+#define DGREP_SHENG_STREAMS 1
+#endif
+#ifndef DGREP_TABLE_STREAMS
+#define DGREP_TABLE_STREAMS 1
+#endif
+#ifndef DGREP_WIDE_STREAMS
+#define DGREP_WIDE_STREAMS 1
+#endif
 #ifndef DGREP_SHENG_WAVES
 #define DGREP_SHENG_WAVES 3
 #endif
 #ifndef DGREP_TABLE_WAVES
 #define DGREP_TABLE_WAVES 3
+#endif
+// staged rounds in flight per wave (1: the next round is fetched while one is
+// stepped; 2: two rounds ahead, double the LDS ring)
+#ifndef DGREP_STAGE_DEPTH
+#define DGREP_STAGE_DEPTH 1
 #endif
 // bytes per lane per staged round (global_load_lds path); 128 = whole lines
 #ifndef DGREP_STAGE_ROUND
@@ -235,17 +249,18 @@ __device__ __forceinline__ StepWide make_step<StepWide>(const uint8_t* lds, cons
 
 template <class Step>
 struct Tune;
+// S = chunks per lane (1, or 2 stepped in lockstep by run_lane2)
 template <>
 struct Tune<StepSheng8> {
-  static constexpr int C = DGREP_SHENG_CHUNK, E = DGREP_SHENG_SLOTS, B = DGREP_SHENG_BLOCK;
+  static constexpr int C = DGREP_SHENG_CHUNK, E = DGREP_SHENG_SLOTS, B = DGREP_SHENG_BLOCK, S = DGREP_SHENG_STREAMS;
 };
 template <>
 struct Tune<StepTable> {
-  static constexpr int C = DGREP_TABLE_CHUNK, E = DGREP_TABLE_SLOTS, B = DGREP_TABLE_BLOCK;
+  static constexpr int C = DGREP_TABLE_CHUNK, E = DGREP_TABLE_SLOTS, B = DGREP_TABLE_BLOCK, S = DGREP_TABLE_STREAMS;
 };
 template <>
 struct Tune<StepWide> {
-  static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK;
+  static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK, S = DGREP_WIDE_STREAMS;
 };
 static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
@@ -307,6 +322,13 @@ struct Blk {
   int lastj;        // its index
 };
 
+// Everything a word step does after its four DFA steps s0..s3 (newline mask
+// m): matching-line events, the first-piece map (TRACK), newline bookkeeping.
+template <int J, bool TRACK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
+                                            uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
+                                            const Emitter<E, DIRECT>& emit);
+
 template <int J, bool TRACK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x, const typename Step::Pre& pre,
                                           uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
@@ -317,6 +339,32 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
   const uint32_t m = nl_mask(x);
   uint32_t s0, s1, s2, s3;
   st.apply(pre, s, s0, s1, s2, s3);
+  word_events<J, TRACK>(st, M, m, pre, s0, s1, s2, s3, b, r, emit);
+  s = s3;
+}
+
+// Two independent chunks per lane stepped in lockstep: both dependency chains
+// are in one basic block (events come after both), so their latencies overlap.
+template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_step2(const Step& st, uint32_t M, uint32_t xa, uint32_t xb,
+                                           const typename Step::Pre& pa, const typename Step::Pre& pb, uint32_t& sa,
+                                           uint32_t& sb, Blk& ba, Blk& bb, LaneRun& ra, LaneRun& rb,
+                                           const Emitter<E, DIRECT>& ea, const Emitter<E, DIRECT>& eb) {
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t ma = nl_mask(xa), mb = nl_mask(xb);
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+  st.apply(pa, sa, a0, a1, a2, a3);
+  st.apply(pb, sb, b0, b1, b2, b3);
+  word_events<J, false>(st, M, ma, pa, a0, a1, a2, a3, ba, ra, ea);
+  word_events<J, false>(st, M, mb, pb, b0, b1, b2, b3, bb, rb, eb);
+  sa = a3;
+  sb = b3;
+}
+
+template <int J, bool TRACK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
+                                            uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
+                                            const Emitter<E, DIRECT>& emit) {
   if (__builtin_expect(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)), 0)) {
     // a '\n' in this word ends a matching line: resolve it exactly
     const uint64_t q0 = b.pos + 4u * J;
@@ -346,19 +394,73 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
   }
   b.nlrun += uint32_t(__popc(m));
   if (m) { b.lastm = m; b.lastj = J; }
-  s = s3;
 }
 
-template <int BK, bool TRACK = false, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
-                                          uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
-  Blk b;
+__device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const LaneRun& r) {
   b.pos = pos;
   b.past = pos >= C;
   b.nl0 = r.nl;
   b.nlrun = 0;
   b.lastm = 0;
   b.lastj = -1;
+}
+
+__device__ __forceinline__ void blk_finish(const Blk& b, uint32_t s, LaneRun& r) {
+  r.s = s;
+  r.nl = b.nl0 + b.nlrun;
+  if (b.lastm) {
+    r.seen = true;
+    r.prev_nl = int64_t(b.pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm));
+    if (b.past) r.term = true;
+  }
+}
+
+// One BK-byte block of each of a lane's two chunks (see word_step2).
+template <int BK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uint4 (&va)[BK / 16],
+                                           const uint4 (&vb)[BK / 16], uint64_t pos, uint64_t C, LaneRun& ra,
+                                           LaneRun& rb, const Emitter<E, DIRECT>& ea, const Emitter<E, DIRECT>& eb) {
+  Blk ba, bb;
+  blk_init(ba, pos, C, ra);
+  blk_init(bb, pos, C, rb);
+  uint32_t sa = ra.s, sb = rb.s;
+  constexpr int NW = BK / 4;
+  uint32_t wa[NW], wb[NW];
+#pragma unroll
+  for (int i = 0; i < BK / 16; ++i) {
+    wa[4 * i + 0] = va[i].x;
+    wa[4 * i + 1] = va[i].y;
+    wa[4 * i + 2] = va[i].z;
+    wa[4 * i + 3] = va[i].w;
+    wb[4 * i + 0] = vb[i].x;
+    wb[4 * i + 1] = vb[i].y;
+    wb[4 * i + 2] = vb[i].z;
+    wb[4 * i + 3] = vb[i].w;
+  }
+  typename Step::Pre pa = st.prep(wa[0]), pb = st.prep(wb[0]);
+#define DG_W2(J)                                                                              \
+  if ((J) < NW) {                                                                             \
+    const typename Step::Pre ca = pa, cb = pb;                                                \
+    if ((J) + 1 < NW) {                                                                       \
+      pa = st.prep(wa[(J) + 1 < NW ? (J) + 1 : 0]);                                           \
+      pb = st.prep(wb[(J) + 1 < NW ? (J) + 1 : 0]);                                           \
+    }                                                                                         \
+    word_step2<J>(st, M, wa[(J) < NW ? (J) : 0], wb[(J) < NW ? (J) : 0], ca, cb, sa, sb, ba, bb, ra, rb, ea, eb); \
+  }
+  DG_W2(0) DG_W2(1) DG_W2(2) DG_W2(3) DG_W2(4) DG_W2(5) DG_W2(6) DG_W2(7)
+  DG_W2(8) DG_W2(9) DG_W2(10) DG_W2(11) DG_W2(12) DG_W2(13) DG_W2(14) DG_W2(15)
+  DG_W2(16) DG_W2(17) DG_W2(18) DG_W2(19) DG_W2(20) DG_W2(21) DG_W2(22) DG_W2(23)
+  DG_W2(24) DG_W2(25) DG_W2(26) DG_W2(27) DG_W2(28) DG_W2(29) DG_W2(30) DG_W2(31)
+#undef DG_W2
+  blk_finish(ba, sa, ra);
+  blk_finish(bb, sb, rb);
+}
+
+template <int BK, bool TRACK = false, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
+                                          uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
+  Blk b;
+  blk_init(b, pos, C, r);
   uint32_t s = r.s;
   // word j's state-independent work (Step::prep) is issued one word ahead
   constexpr int NW = BK / 4;
@@ -382,13 +484,7 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
   DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
 #undef DG_W
-  r.s = s;
-  r.nl = b.nl0 + b.nlrun;
-  if (b.lastm) {
-    r.seen = true;
-    r.prev_nl = int64_t(pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm));
-    if (b.past) r.term = true;
-  }
+  blk_finish(b, s, r);
 }
 
 template <int BK>
@@ -479,6 +575,38 @@ __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, 
   return run_lane_from<C, BK>(a, st, cs, 0, r, emit);
 }
 
+// Two chunks per lane (csa, csb), both wholly inside the split, stepped in
+// lockstep over [0, C) with direct loads (two independent dependency chains
+// per lane); then each finishes its last owned line on its own.
+template <int C, int BK, class Step, int E>
+__device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uint64_t csa, uint64_t csb, LaneRun& ra,
+                                          LaneRun& rb, const Emitter<E, false>& ea, const Emitter<E, false>& eb,
+                                          uint32_t& nla, uint32_t& nlb) {
+  static_assert(C % (2 * BK) == 0, "chunk must hold an even number of blocks");
+  const uint32_t M = a.start_m;
+  lane_init(a, csa, ra);
+  lane_init(a, csb, rb);
+  const uint8_t* pa = a.data + csa;
+  const uint8_t* pb = a.data + csb;
+  uint4 A0[BK / 16], A1[BK / 16], B0[BK / 16], B1[BK / 16];
+  load_block<BK>(A0, pa);
+  load_block<BK>(B0, pb);
+  for (uint32_t pos = 0; pos < uint32_t(C); pos += 2 * BK) {
+    load_block<BK>(A1, pa + pos + BK);
+    load_block<BK>(B1, pb + pos + BK);
+    run_block2<BK>(st, M, A0, B0, pos, uint64_t(C), ra, rb, ea, eb);
+    if (pos + 2 * BK < uint32_t(C)) {
+      load_block<BK>(A0, pa + pos + 2 * BK);
+      load_block<BK>(B0, pb + pos + 2 * BK);
+    }
+    run_block2<BK>(st, M, A1, B1, pos + BK, uint64_t(C), ra, rb, ea, eb);
+  }
+  nla = ra.nl;
+  nlb = rb.nl;
+  run_lane_from<C, BK>(a, st, csa, uint64_t(C), ra, ea);
+  run_lane_from<C, BK>(a, st, csb, uint64_t(C), rb, eb);
+}
+
 // 16 bytes global -> LDS (global_load_lds_dwordx4); the LDS destination is
 // the wave-uniform `lds` + lane * 16. (The builtin exists only in the device
 // compilation pass; the host pass never executes device code.)
@@ -513,18 +641,32 @@ __device__ __forceinline__ uint32_t run_lane_staged(const ScanArgs& a, const Ste
   const uint8_t* rd = stage + (lane / SPI) * 1024 + 16 * ((lane % SPI) * P);
   const int fl = (lane / G) % P;
   constexpr bool kTrack = Step::kKind == kStepSheng8;
+  constexpr int D = DGREP_STAGE_DEPTH, RB = 64 * R;  // rounds in flight, bytes per round buffer
+  static_assert(D == 1 || D == 2, "stage depth 1 or 2");
 #pragma unroll
-  for (int k = 0; k < P; ++k) glds16(tb + off[k], stage + k * 1024);
+  for (int d = 0; d < D; ++d) {
+    if (d < NR) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) glds16(tb + off[k] + uint32_t(d) * uint32_t(R), stage + d * RB + k * 1024);
+    }
+  }
   for (int rr = 0; rr < NR; ++rr) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // round rr has landed when only the P loads of round rr+1 (depth 2) may still be pending
+    if (D == 2 && rr + 1 < NR) {
+      if constexpr (P == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const int buf = D == 2 ? (rr & 1) : 0;
     uint4 v[P];
 #pragma unroll
-    for (int j = 0; j < P; ++j) v[j] = *reinterpret_cast<const uint4*>(rd + 16 * (j ^ fl));
+    for (int j = 0; j < P; ++j) v[j] = *reinterpret_cast<const uint4*>(rd + buf * RB + 16 * (j ^ fl));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (rr + 1 < NR) {
+    if (rr + D < NR) {
 #pragma unroll
       for (int k = 0; k < P; ++k)
-        glds16(tb + off[k] + uint32_t(rr + 1) * uint32_t(R), stage + k * 1024);
+        glds16(tb + off[k] + uint32_t(rr + D) * uint32_t(R), stage + buf * RB + k * 1024);
     }
     run_block<R, kTrack>(st, M, v, uint64_t(rr) * R, uint64_t(C), r, emit);
   }
@@ -580,42 +722,62 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
   constexpr bool kStaged = use_staging<Step, TBL>();
   constexpr int R = DGREP_STAGE_ROUND;
-  __shared__ ScanSmem<TBL, E, NT> sm;
+  __shared__ ScanSmem<TBL, E * Tune<Step>::S, NT> sm;
   // the staging rings are a __shared__ object of their own: with the table in
   // the same object, hipcc cannot tell a ring write (global_load_lds) from a
   // table read and drains vmcnt before every table lookup
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kStaged ? (NT / 64) * 64 * R : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kStaged ? (NT / 64) * DGREP_STAGE_DEPTH * 64 * R : 16];
   const int tid = int(threadIdx.x);
   for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += NT * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
   __syncthreads();
 
   const Step st = make_step<Step>(sm.tbl, a);
-  uint32_t* slots = sm.slots + tid * E * 2;
+  constexpr int S = Tune<Step>::S;  // chunks per lane: chunk k of a tile is k * 64 + lane
+  uint32_t* slots = sm.slots + tid * S * E * 2;
   const int lane = tid & 63;
   const uint64_t waves = uint64_t(gridDim.x) * (NT / 64);
+  constexpr uint64_t kTile = uint64_t(kTileLanes) * uint64_t(S) * uint64_t(C);
   for (uint64_t t = uint64_t(blockIdx.x) * (NT / 64) + uint64_t(tid >> 6); t < a.ntiles; t += waves) {
-    const uint64_t cs = t * uint64_t(kTileLanes) * uint64_t(C) + uint64_t(lane) * uint64_t(C);
-    LaneRun r;
-    Emitter<E, false> em{&a, slots, cs, 0, 0};
-    uint32_t nlc;
-    if constexpr (kStaged) {
-      // wave-uniform: the whole tile lies inside the split
-      if ((t + 1) * uint64_t(kTileLanes) * uint64_t(C) <= a.n)
-        nlc = run_lane_staged<C, R>(a, st, cs, lane, stage + (tid >> 6) * (64 * R), r, em);
-      else
-        nlc = run_lane<C, BK>(a, st, cs, r, em);
+    uint64_t cs[S];
+    LaneRun r[S];
+    uint32_t nlc[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) cs[k] = t * kTile + (uint64_t(k) * kTileLanes + uint64_t(lane)) * uint64_t(C);
+    const bool full = (t + 1) * kTile <= a.n;  // wave-uniform: the whole tile lies inside the split
+    if constexpr (S == 2) {
+      const Emitter<E, false> e0{&a, slots, cs[0], 0, 0}, e1{&a, slots + E * 2, cs[1], 0, 0};
+      if (full) {
+        run_lane2<C, BK>(a, st, cs[0], cs[1], r[0], r[1], e0, e1, nlc[0], nlc[1]);
+      } else {
+        nlc[0] = run_lane<C, BK>(a, st, cs[0], r[0], e0);
+        nlc[1] = run_lane<C, BK>(a, st, cs[1], r[1], e1);
+      }
     } else {
-      nlc = run_lane<C, BK>(a, st, cs, r, em);
+      const Emitter<E, false> em{&a, slots, cs[0], 0, 0};
+      if constexpr (kStaged) {
+        if (full)
+          nlc[0] = run_lane_staged<C, R>(a, st, cs[0], lane, stage + (tid >> 6) * (DGREP_STAGE_DEPTH * 64 * R), r[0],
+                                         em);
+        else
+          nlc[0] = run_lane<C, BK>(a, st, cs[0], r[0], em);
+      } else {
+        nlc[0] = run_lane<C, BK>(a, st, cs[0], r[0], em);
+      }
     }
-    const uint32_t nev = r.nev;
 
-    // tile-wide exclusive scans of (newlines, matching lines) across the wave
-    const uint32_t nl_inc = wave_incl_scan(nlc);
-    const uint32_t ev_inc = wave_incl_scan(nev);
-    const uint32_t nl_tot = __shfl(nl_inc, 63, 64);
-    const uint32_t ev_tot = __shfl(ev_inc, 63, 64);
-    const uint32_t nl_off = nl_inc - nlc, ev_off = ev_inc - nev;
+    // tile-wide exclusive scans of (newlines, matching lines) over the tile's
+    // chunks in split order (stream 0's 64 chunks, then stream 1's)
+    uint32_t nl_off[S], ev_off[S], nl_tot = 0, ev_tot = 0;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const uint32_t nl_inc = wave_incl_scan(nlc[k]);
+      const uint32_t ev_inc = wave_incl_scan(r[k].nev);
+      nl_off[k] = nl_tot + nl_inc - nlc[k];
+      ev_off[k] = ev_tot + ev_inc - r[k].nev;
+      nl_tot += __shfl(nl_inc, 63, 64);
+      ev_tot += __shfl(ev_inc, 63, 64);
+    }
     unsigned long long base = 0;
     if (lane == 0) {
       if (ev_tot) base = atomicAdd(a.counter, (unsigned long long)ev_tot);
@@ -627,30 +789,35 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
     }
     if (ev_tot == 0) continue;  // wave-uniform
     base = (uint64_t(uint32_t(__shfl(uint32_t(base >> 32), 0, 64))) << 32) | uint32_t(__shfl(uint32_t(base), 0, 64));
-    const uint64_t o0 = base + ev_off;
-    if (nev <= uint32_t(E)) {
-      for (uint32_t k = 0; k < nev; ++k) {
-        const uint64_t o = o0 + k;
-        if (o < a.capacity) {
-          const uint32_t w0 = slots[k * 2 + 0];
-          StagedLine L;
-          L.start = cs + (w0 & 0xffffu);
-          L.len = slots[k * 2 + 1];
-          L.rel = nl_off + (w0 >> 16);
-          a.staging[o] = L;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const uint32_t nev = r[k].nev;
+      const uint32_t* sl = slots + k * E * 2;
+      const uint64_t o0 = base + ev_off[k];
+      if (nev <= uint32_t(E)) {
+        for (uint32_t j = 0; j < nev; ++j) {
+          const uint64_t o = o0 + j;
+          if (o < a.capacity) {
+            const uint32_t w0 = sl[j * 2 + 0];
+            StagedLine L;
+            L.start = cs[k] + (w0 & 0xffffu);
+            L.len = sl[j * 2 + 1];
+            L.rel = nl_off[k] + (w0 >> 16);
+            a.staging[o] = L;
+          }
         }
-      }
-    } else {
-      // more matching lines than LDS slots: scan_overflow_kernel re-runs
-      // this lane and writes straight to its final staging positions
-      const unsigned long long k = atomicAdd(a.overflow_count, 1ull);
-      if (k < a.overflow_cap) {
-        OverflowLane ol;
-        ol.cs = cs;
-        ol.out_base = o0;
-        ol.nl_prefix = nl_off;
-        ol.pad = 0;
-        a.overflow[k] = ol;
+      } else {
+        // more matching lines than LDS slots: scan_overflow_kernel re-runs
+        // this chunk and writes straight to its final staging positions
+        const unsigned long long q = atomicAdd(a.overflow_count, 1ull);
+        if (q < a.overflow_cap) {
+          OverflowLane ol;
+          ol.cs = cs[k];
+          ol.out_base = o0;
+          ol.nl_prefix = nl_off[k];
+          ol.pad = 0;
+          a.overflow[q] = ol;
+        }
       }
     }
   }
@@ -779,8 +946,9 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
 // ---- host-side launchers (called from dgrep_runtime.cpp) ----------------
 
 uint64_t scan_tile_bytes(int kind) {
-  const int C = kind == kStepSheng8 ? Tune<StepSheng8>::C : kind == kStepWide ? Tune<StepWide>::C : Tune<StepTable>::C;
-  return uint64_t(kTileLanes) * uint64_t(C);
+  if (kind == kStepSheng8) return uint64_t(kTileLanes) * Tune<StepSheng8>::S * Tune<StepSheng8>::C;
+  if (kind == kStepWide) return uint64_t(kTileLanes) * Tune<StepWide>::S * Tune<StepWide>::C;
+  return uint64_t(kTileLanes) * Tune<StepTable>::S * Tune<StepTable>::C;
 }
 uint32_t scan_table_row() { return kRow; }
 
