@@ -217,10 +217,14 @@ def main():
 
 
 def verify_windows(buf, n, line_t, start_t, len_t, pattern, k, win):
-    """Parity at full size: random whole-line windows of the split re-run on the
+    """Parity at full size: k whole-line windows, evenly spaced so that the
+    first and the last always sit at the split's start and end, re-run on the
     oracle (lines renumbered by the '\\n' count before the window, counted on the
-    GPU) must equal the GPU records inside the window; records must be strictly
-    ascending."""
+    GPU) must equal the GPU records inside the window. Every record (not only
+    those in windows) must be a whole line -- preceded by '\\n' or the split
+    start, followed by '\\n' or the split end -- whose line number is 1 + the
+    number of '\\n' before it (searchsorted over the GPU's newline positions),
+    and records must be strictly ascending."""
     import numpy as np
     import torch
 
@@ -229,10 +233,11 @@ def verify_windows(buf, n, line_t, start_t, len_t, pattern, k, win):
 
     if line_t.numel() > 1:
         assert bool((line_t[1:] > line_t[:-1]).all()), "line numbers not strictly ascending"
-    rng = np.random.default_rng(12345)
+    check_records(buf, n, line_t, start_t, len_t)
     ok = 0
-    for _ in range(k):
-        a0 = int(rng.integers(0, max(1, n - win)))
+    span = max(0, n - win)
+    for w in range(k):
+        a0 = (span * w) // max(1, k - 1) if k > 1 else 0
         chunk = buf[a0:min(n, a0 + win)].cpu().numpy().tobytes()
         i = chunk.find(b"\n")
         j = chunk.rfind(b"\n")
@@ -252,6 +257,29 @@ def verify_windows(buf, n, line_t, start_t, len_t, pattern, k, win):
         ok += 1
         log("verified window %d/%d at byte %d (%d matching lines)" % (ok, k, a, len(oln)))
     return ok
+
+
+def check_records(buf, n, line_t, start_t, len_t):
+    """Structural check of every GPU record on the GPU (see verify_windows)."""
+    import torch
+
+    if line_t.numel() == 0:
+        return
+    st = start_t.to(torch.int64)
+    en = st + len_t.to(torch.int64) % (1 << 32)
+    assert bool((st >= 0).all()) and bool((en <= n).all()), "record outside the split"
+    step = 1 << 30  # torch.nonzero mis-sizes its output past 2**31 elements: 1 GiB pieces
+    nlpos = torch.cat([torch.nonzero(buf[o:min(n, o + step)] == 10).flatten() + o for o in range(0, n, step)])
+    prev_ok = (st == 0) | (buf[(st - 1).clamp(min=0)] == 10)
+    end_ok = (en == n) | (buf[en.clamp(max=n - 1)] == 10)
+    assert bool(prev_ok.all()), "a record does not start at a line start"
+    assert bool(end_ok.all()), "a record does not end at a line end"
+    nl_in = torch.searchsorted(nlpos, en) - torch.searchsorted(nlpos, st)
+    assert bool((nl_in == 0).all()), "a record spans a newline"
+    want = torch.searchsorted(nlpos, st) + 1
+    assert bool((line_t.to(torch.int64) == want).all()), "line numbers disagree with the newline count"
+    del nlpos
+    log("checked %d records: whole lines, numbering consistent" % line_t.numel())
 
 
 def cpu_baseline(buf, n, pattern, seconds):

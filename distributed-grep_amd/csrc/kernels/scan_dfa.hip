@@ -49,7 +49,8 @@
 //   WAVES    waves per SIMD the register allocation must allow
 // Sheng (C2, 7 states): direct per-lane loads, 4 KiB chunks, 128-B blocks:
 // 4.16-4.22 TB/s; the staged variant measured 3.5-3.8 TB/s at 1-2 KiB chunks.
-// Table (C3, 20 states): staged, 2 KiB chunks: 2.83 TB/s (direct 2.67).
+// Table (C3, 20 states): two 2 KiB chunks per lane stepped in lockstep, direct
+// loads: 2.94 TB/s (one chunk staged 2.83, direct 2.67).
 #ifndef DGREP_SHENG_CHUNK
 #define DGREP_SHENG_CHUNK 4096
 #endif
@@ -69,13 +70,13 @@
 #define DGREP_TABLE_SLOTS 6
 #endif
 #ifndef DGREP_TABLE_STAGING
-#define DGREP_TABLE_STAGING 1
+#define DGREP_TABLE_STAGING 0
 #endif
 #ifndef DGREP_SHENG_STREAMS
 #define DGREP_SHENG_STREAMS 1
 #endif
 #ifndef DGREP_TABLE_STREAMS
-#define DGREP_TABLE_STREAMS 1
+#define DGREP_TABLE_STREAMS 2
 #endif
 #ifndef DGREP_WIDE_STREAMS
 #define DGREP_WIDE_STREAMS 1
@@ -266,6 +267,14 @@ static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block mu
 static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>::C % Tune<StepTable>::B == 0,
               "chunk must be a multiple of the block");
+
+// chunks per lane: the table stepper runs two in lockstep while its table is
+// small (<= 64 states); a bigger table would lose more occupancy (the LDS
+// slots double) than the second dependency chain gains
+template <class Step, int TBL>
+constexpr int streams_of() {
+  return Step::kKind == kStepTable ? (TBL <= 64 * int(kRow) ? Tune<Step>::S : 1) : Tune<Step>::S;
+}
 
 // Per-lane run state. Positions are relative to the lane's chunk start `cs`.
 struct LaneRun {
@@ -722,7 +731,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
   constexpr bool kStaged = use_staging<Step, TBL>();
   constexpr int R = DGREP_STAGE_ROUND;
-  __shared__ ScanSmem<TBL, E * Tune<Step>::S, NT> sm;
+  __shared__ ScanSmem<TBL, E * streams_of<Step, TBL>(), NT> sm;
   // the staging rings are a __shared__ object of their own: with the table in
   // the same object, hipcc cannot tell a ring write (global_load_lds) from a
   // table read and drains vmcnt before every table lookup
@@ -733,7 +742,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   __syncthreads();
 
   const Step st = make_step<Step>(sm.tbl, a);
-  constexpr int S = Tune<Step>::S;  // chunks per lane: chunk k of a tile is k * 64 + lane
+  constexpr int S = streams_of<Step, TBL>();  // chunks per lane: chunk k of a tile is k * 64 + lane
   uint32_t* slots = sm.slots + tid * S * E * 2;
   const int lane = tid & 63;
   const uint64_t waves = uint64_t(gridDim.x) * (NT / 64);
@@ -945,11 +954,6 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
 
 // ---- host-side launchers (called from dgrep_runtime.cpp) ----------------
 
-uint64_t scan_tile_bytes(int kind) {
-  if (kind == kStepSheng8) return uint64_t(kTileLanes) * Tune<StepSheng8>::S * Tune<StepSheng8>::C;
-  if (kind == kStepWide) return uint64_t(kTileLanes) * Tune<StepWide>::S * Tune<StepWide>::C;
-  return uint64_t(kTileLanes) * Tune<StepTable>::S * Tune<StepTable>::C;
-}
 uint32_t scan_table_row() { return kRow; }
 
 namespace {
@@ -985,6 +989,14 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (table_bytes <= 128 * kRow) return op.template run<StepTable, 128 * kRow>();
   return op.template run<StepTable, 256 * kRow>();
 }
+struct TileOp {
+  uint64_t* bytes;
+  template <class S, int T>
+  hipError_t run() const {
+    *bytes = uint64_t(kTileLanes) * uint64_t(streams_of<S, T>()) * uint64_t(Tune<S>::C);
+    return hipSuccess;
+  }
+};
 struct OccOp {
   int* b;
   template <class S, int T>
@@ -1006,6 +1018,11 @@ struct OverflowOp {
 };
 }  // namespace
 
+uint64_t scan_tile_bytes(int kind, uint32_t table_bytes) {
+  uint64_t b = 0;
+  (void)dispatch(kind, table_bytes, TileOp{&b});
+  return b;
+}
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {
   return dispatch(kind, table_bytes, OccOp{blocks_per_cu});
 }

@@ -18,9 +18,15 @@
 #include "../kernels/scan_common.h"
 #include "../kernels/synth.h"
 
+// DFAs of at most this many states use the Sheng stepper (8 = its limit; 0
+// sends every DFA of <= 256 states to the table stepper)
+#ifndef DGREP_SHENG_MAX_STATES
+#define DGREP_SHENG_MAX_STATES 8
+#endif
+
 namespace dgrep {
 // scan_dfa.hip
-uint64_t scan_tile_bytes(int kind);
+uint64_t scan_tile_bytes(int kind, uint32_t table_bytes);
 uint32_t scan_table_row();
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu);
 hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
@@ -206,7 +212,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     t.assign((kWideClassBytes + size_t(c->hot_entries) * 2 + 15) & ~size_t(15), 0);
     memcpy(t.data(), h.byte_class, 256);
     memcpy(t.data() + kWideClassBytes, wide.data(), size_t(c->hot_entries) * 2);
-  } else if (h.nstates <= 8) {
+  } else if (h.nstates <= DGREP_SHENG_MAX_STATES) {
     // StepSheng8: V[b] = 8 bytes, byte s = next state of s on input byte b
     c->step_kind = kStepSheng8;
     t.assign(256 * 8, 0);
@@ -268,7 +274,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     c->err = "device split must be 16-byte aligned";
     return DGREP_E_INVALID;
   }
-  const uint64_t tile = scan_tile_bytes(c->step_kind);
+  const uint64_t tile = scan_tile_bytes(c->step_kind, c->table_bytes);
   const uint64_t ntiles = (n + tile - 1) / tile;
   int rc;
   if ((rc = grow(c, &c->d_tiles, &c->tiles_cap, ntiles)) != DGREP_OK) return rc;

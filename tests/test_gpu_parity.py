@@ -102,6 +102,26 @@ def test_tile_and_chunk_boundaries(gpu_ctx, size):
         _check(gpu_ctx, pattern, data)
 
 
+# table-stepper instantiations: <= 64 states run two chunks per lane (tile 256
+# KiB), 65-256 states one (tile 128 KiB); both at their chunk and tile edges
+@pytest.mark.parametrize("pattern", [b"(alpha|bravo|charlie|delta|echo|foxtrot|golf|hotel|india|juliet)[0-9]+",
+                                     b"(alpha|bravo|charlie|delta|echo|foxtrot|golf|hotel|india|juliet|kilo|lima|"
+                                     b"mike|november|oscar|papa|quebec|romeo)"])
+def test_table_stream_configs_at_edges(gpu_ctx, pattern):
+    import dgrep
+
+    rnd = random.Random(7)
+    words = [b"alpha", b"bravo7", b"romeo", b"x", b"juliet12", b"error", b" ", b"  ", b"quebec", b"kilo9"]
+    for size in (2047, 2048, 2049, 131071, 131072, 131073, 262143, 262144, 262145, 5 * 131072 + 33):
+        data = bytearray(b"".join(rnd.choice(words) for _ in range(size // 3))[:size])
+        for edge in (2047, 2048, 4095, 4096, 131071, 131072, 262143, 262144):
+            if edge < len(data):
+                data[edge] = 0x0A
+        cp = gpu_ctx.load(pattern)
+        assert 8 < cp.nstates <= 256
+        _check(gpu_ctx, cp, bytes(data))
+
+
 def test_long_lines_cross_many_chunks(gpu_ctx):
     rnd = random.Random(3)
     parts = []
