@@ -70,7 +70,10 @@ enum : int {
 // start), so the shallow states an Aho-Corasick-like automaton spends nearly
 // all its steps in are LDS-resident and the deep ones are read from L2.
 constexpr uint32_t kWideClassBytes = 256;
-constexpr uint32_t kWideHotBytes = 96 * 1024;
+#ifndef DGREP_WIDE_HOT_KIB
+#define DGREP_WIDE_HOT_KIB 96
+#endif
+constexpr uint32_t kWideHotBytes = DGREP_WIDE_HOT_KIB * 1024;
 constexpr int kWideThreads = 1024;  // one workgroup per CU shares one LDS copy
 
 }  // namespace dgrep

@@ -10,7 +10,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/dgrep.h"
@@ -83,6 +85,20 @@ struct dgrep_ctx {
 
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
+
+  // dgrep_scan ingest (worker split -> HBM): host bytes are copied by
+  // `ingest_threads` CPU threads into one of `ingest_bufs` pinned staging
+  // buffers of `ingest_chunk` bytes while the copy engine DMAs the previous
+  // one to HBM on `copy_stream` (dgrep_set_ingest; chunk 0 = one direct
+  // pageable hipMemcpyAsync)
+  size_t ingest_chunk = size_t(64) << 20;
+  int ingest_bufs = 4;
+  int ingest_threads = 4;
+  std::vector<uint8_t*> h_stage;
+  std::vector<hipEvent_t> ev_stage;
+  size_t stage_bytes = 0;
+  hipStream_t copy_stream = nullptr;
+  float last_ingest_ms = 0.f;
 };
 
 namespace {
@@ -140,6 +156,12 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  for (uint8_t* h : c->h_stage)
+    if (h) (void)hipHostFree(h);
+  for (hipEvent_t e : c->ev_stage)
+    if (e) (void)hipEventDestroy(e);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -342,6 +364,88 @@ extern "C" int dgrep_scan_device(dgrep_ctx* c, const void* d_data, size_t n, uin
   return scan_resident(c, static_cast<const uint8_t*>(d_data), n, d_line_no, d_start, d_len, capacity, count);
 }
 
+// Worker-side ingest of one split (the bytes map_reduce/worker.go:72-76
+// read with os.ReadFile and hand to Map): host -> pinned staging -> HBM.
+// Piece k is memcpy'd by the CPU threads into staging buffer k % B once the
+// DMA that last read that buffer has finished, then DMA'd on the copy stream;
+// so the CPU copy of piece k+1 overlaps the DMA of piece k. The scan stream
+// waits on the last DMA. A split of at most one piece below 4 MiB, or chunk
+// 0, takes one pageable hipMemcpyAsync instead.
+static int ingest(dgrep_ctx* c, const uint8_t* data, size_t n) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (c->ingest_chunk == 0 || n < (size_t(4) << 20)) {
+    HIPCHK(hipMemcpyAsync(c->d_data, data, n, hipMemcpyHostToDevice, c->stream));
+    c->last_ingest_ms = 0.f;
+    return DGREP_OK;
+  }
+  const size_t S = c->ingest_chunk;
+  const int B = std::max(2, c->ingest_bufs);
+  if (c->stage_bytes != S || int(c->h_stage.size()) != B) {
+    if (c->copy_stream) HIPCHK(hipStreamSynchronize(c->copy_stream));
+    for (uint8_t* h : c->h_stage)
+      if (h) HIPCHK(hipHostFree(h));
+    for (hipEvent_t e : c->ev_stage)
+      if (e) HIPCHK(hipEventDestroy(e));
+    c->h_stage.assign(B, nullptr);
+    c->ev_stage.assign(B, nullptr);
+    c->stage_bytes = 0;
+    for (int b = 0; b < B; ++b) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_stage[b]), S, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&c->ev_stage[b], hipEventDisableTiming));
+    }
+    c->stage_bytes = S;
+  }
+  if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  // the previous scan may still read d_data: the first DMA waits for it
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev1, 0));
+  const int T = std::max(1, c->ingest_threads);
+  std::vector<bool> used(B, false);
+  const size_t pieces = (n + S - 1) / S;
+  for (size_t k = 0; k < pieces; ++k) {
+    const int b = int(k % size_t(B));
+    const size_t off = k * S, len = std::min(S, n - off);
+    if (used[b]) HIPCHK(hipEventSynchronize(c->ev_stage[b]));  // buffer b's last DMA is done
+    uint8_t* dst = c->h_stage[b];
+    const uint8_t* src = data + off;
+    if (T == 1 || len < (size_t(1) << 20)) {
+      memcpy(dst, src, len);
+    } else {
+      std::vector<std::thread> th;
+      const size_t part = ((len + T - 1) / T + 4095) & ~size_t(4095);
+      for (int t = 0; t < T; ++t) {
+        const size_t a = size_t(t) * part;
+        if (a >= len) break;
+        const size_t m = std::min(part, len - a);
+        th.emplace_back([=] { memcpy(dst + a, src + a, m); });
+      }
+      for (auto& x : th) x.join();
+    }
+    HIPCHK(hipMemcpyAsync(c->d_data + off, dst, len, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipEventRecord(c->ev_stage[b], c->copy_stream));
+    used[b] = true;
+  }
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_stage[int((pieces - 1) % size_t(B))], 0));
+  HIPCHK(hipStreamSynchronize(c->copy_stream));
+  c->last_ingest_ms =
+      std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_set_ingest(dgrep_ctx* c, size_t chunk_bytes, int nbufs, int threads) {
+  if (!c || nbufs < 0 || threads < 0 || nbufs > 64 || threads > 256) return DGREP_E_INVALID;
+  c->ingest_chunk = chunk_bytes;
+  if (nbufs) c->ingest_bufs = nbufs;
+  if (threads) c->ingest_threads = threads;
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_last_ingest_ms(dgrep_ctx* c, float* ms) {
+  if (!c || !ms) return DGREP_E_INVALID;
+  *ms = c->last_ingest_ms;
+  return DGREP_OK;
+}
+
 extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_result* out) {
   if (!c || !out || (n && !data)) return DGREP_E_INVALID;
   memset(out, 0, sizeof *out);
@@ -352,7 +456,7 @@ extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_res
     uint64_t cap = c->data_cap;
     if ((rc = grow(c, &c->d_data, &cap, (n + 63) & ~uint64_t(63))) != DGREP_OK) return rc;
     c->data_cap = cap;
-    HIPCHK(hipMemcpyAsync(c->d_data, data, n, hipMemcpyHostToDevice, c->stream));
+    if ((rc = ingest(c, data, n)) != DGREP_OK) return rc;
   }
   uint64_t want = std::max<uint64_t>(c->res_cap, std::max<uint64_t>(1024, n / 512));
   uint64_t count = 0;

@@ -51,7 +51,7 @@ EXPORTS = (
     "dgrep_compile", "dgrep_blob_free", "dgrep_blob_info_get", "dgrep_open", "dgrep_close",
     "dgrep_last_error", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
-    "dgrep_last_kernel_ms", "dgrep_set_stepper",
+    "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_ingest", "dgrep_last_ingest_ms",
 )
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
@@ -122,6 +122,10 @@ def lib() -> ctypes.CDLL:
             L.dgrep_synth_keyword.restype = i
             L.dgrep_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
             L.dgrep_last_kernel_ms.restype = i
+            L.dgrep_set_ingest.argtypes = [vp, sz, i, i]
+            L.dgrep_set_ingest.restype = i
+            L.dgrep_last_ingest_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+            L.dgrep_last_ingest_ms.restype = i
             _lib = L
     return _lib
 
@@ -245,6 +249,17 @@ class Context:
 
     def synth(self, d_out: int, n: int, seed: int, kind: int = 0):
         self._check(self._L.dgrep_synth_corpus(self._h, ctypes.c_void_p(d_out), n, seed, kind))
+
+    def set_ingest(self, chunk_bytes: int, nbufs: int = 0, threads: int = 0):
+        """Ingest pipeline of scan(): pinned staging pieces of chunk_bytes (0 =
+        one direct pageable copy), nbufs buffers, threads host-copy threads
+        (dgrep_set_ingest; 0 keeps the current value)."""
+        self._check(self._L.dgrep_set_ingest(self._h, chunk_bytes, nbufs, threads))
+
+    def last_ingest_ms(self) -> float:
+        ms = ctypes.c_float()
+        self._check(self._L.dgrep_last_ingest_ms(self._h, ctypes.byref(ms)))
+        return float(ms.value)
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()

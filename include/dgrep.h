@@ -97,8 +97,20 @@ int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
  * wide_hot_rows != 0 caps its LDS-resident rows. */
 int dgrep_set_stepper(dgrep_ctx* ctx, int force_wide, uint32_t wide_hot_rows);
 
-/* Host bytes -> H2D -> scan -> D2H results. This is the call Map makes. */
+/* Host bytes -> H2D -> scan -> D2H results. This is the call Map makes.
+ * The H2D leg is the worker's split ingest (the bytes map_reduce/worker.go:72-76
+ * reads with os.ReadFile and passes to Map at worker.go:141): pieces are
+ * copied by CPU threads into pinned staging buffers while the copy engine
+ * DMAs the previous piece (dgrep_set_ingest). */
 int dgrep_scan(dgrep_ctx* ctx, const uint8_t* data, size_t n, dgrep_result* out);
+/* Ingest pipeline of dgrep_scan: chunk_bytes per pinned staging buffer
+ * (0 = one pageable hipMemcpyAsync, no staging), nbufs buffers in rotation,
+ * threads CPU threads per piece copy (0 keeps the current value). Defaults:
+ * 64 MiB x 4 buffers x 4 threads. */
+int dgrep_set_ingest(dgrep_ctx* ctx, size_t chunk_bytes, int nbufs, int threads);
+/* Wall time (ms) of the last dgrep_scan's ingest (host -> HBM), 0 for the
+ * direct path. */
+int dgrep_last_ingest_ms(dgrep_ctx* ctx, float* ms);
 void dgrep_result_free(dgrep_result* r);
 
 /* HBM-resident split (the data never leaves the device): results are written

@@ -182,6 +182,44 @@ def test_scan_device_resident(gpu_ctx):
     assert cnt2 == cnt
 
 
+@pytest.mark.parametrize("chunk,bufs,threads", [(1 << 20, 2, 1), ((1 << 20) + 4097, 3, 4), (8 << 20, 4, 8)])
+def test_ingest_pipeline_bit_exact(chunk, bufs, threads):
+    """dgrep_scan's pinned-staging ingest (pieces of `chunk` bytes through
+    `bufs` rotating buffers) lands the split in HBM byte for byte: same
+    records as the direct copy and as the oracle, across piece boundaries."""
+    import dgrep
+
+    data = bytearray(dgrep.synth_corpus_host(20 << 20, 5, 0))
+    for k in range(1, 20):  # lines ending exactly at piece edges
+        e = k * chunk
+        if e < len(data):
+            data[e - 1] = 0x0A
+    data = bytes(data)
+    ctx = dgrep.Context(0)
+    try:
+        for pattern in (b"error", b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+"):
+            ctx.load(pattern)
+            ctx.set_ingest(0)
+            want = ctx.scan(data)
+            ctx.set_ingest(chunk, bufs, threads)
+            got = ctx.scan(data)
+            assert ctx.last_ingest_ms() > 0
+            for g, w in zip(got, want):
+                np.testing.assert_array_equal(g, w)
+            oln, ost, ole = _oracle(pattern, data, 16)
+            np.testing.assert_array_equal(got[0], oln)
+            np.testing.assert_array_equal(got[1], ost)
+            np.testing.assert_array_equal(got[2], ole)
+            # a second, shorter split reuses the staging buffers
+            short = data[: (5 << 20) + 3]
+            got2 = ctx.scan(short)
+            o2 = _oracle(pattern, short, 16)
+            np.testing.assert_array_equal(got2[0], o2[0])
+            np.testing.assert_array_equal(got2[1], o2[1])
+    finally:
+        ctx.close()
+
+
 def test_map_reduce_surface(gpu_ctx):
     import dgrep
 
