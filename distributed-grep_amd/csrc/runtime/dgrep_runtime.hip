@@ -17,6 +17,7 @@
 
 #include "../../../include/dgrep.h"
 #include "../../../include/dgrep_blob.h"
+#include "../kernels/encode.h"
 #include "../kernels/scan_common.h"
 #include "../kernels/synth.h"
 
@@ -99,6 +100,17 @@ struct dgrep_ctx {
   size_t stage_bytes = 0;
   hipStream_t copy_stream = nullptr;
   float last_ingest_ms = 0.f;
+
+  // partition + intermediate writer (dgrep_encode_device / dgrep_map_partitions)
+  uint8_t* d_enc_scratch = nullptr;
+  uint64_t enc_scratch_cap = 0;
+  uint8_t* d_fname = nullptr;
+  uint64_t fname_cap = 0;
+  uint64_t* d_bounds = nullptr;
+  uint64_t bounds_cap = 0;
+  uint8_t* d_enc_out = nullptr;
+  uint64_t enc_out_cap = 0;
+  float last_encode_ms = 0.f;
 };
 
 namespace {
@@ -153,7 +165,8 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_table, c->d_wide, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
-                  c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len};
+                  c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
+                  c->d_fname, c->d_bounds, c->d_enc_out};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -446,11 +459,8 @@ extern "C" int dgrep_last_ingest_ms(dgrep_ctx* c, float* ms) {
   return DGREP_OK;
 }
 
-extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_result* out) {
-  if (!c || !out || (n && !data)) return DGREP_E_INVALID;
-  memset(out, 0, sizeof *out);
-  if (!c->loaded) { c->err = "no DFA loaded"; return DGREP_E_NO_DFA; }
-  HIPCHK(hipSetDevice(c->device));
+// Host split -> HBM (ingest) -> scan into the context's result arrays.
+static int scan_host(dgrep_ctx* c, const uint8_t* data, size_t n, uint64_t* count) {
   int rc;
   if (n) {
     uint64_t cap = c->data_cap;
@@ -459,7 +469,6 @@ extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_res
     if ((rc = ingest(c, data, n)) != DGREP_OK) return rc;
   }
   uint64_t want = std::max<uint64_t>(c->res_cap, std::max<uint64_t>(1024, n / 512));
-  uint64_t count = 0;
   for (int attempt = 0; attempt < 2; ++attempt) {
     if (want > c->res_cap) {
       uint64_t c1 = 0, c2 = 0, c3 = 0;
@@ -471,12 +480,23 @@ extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_res
       if ((rc = grow(c, &c->d_res_len, &c3, want)) != DGREP_OK) return rc;
       c->res_cap = want;
     }
-    if ((rc = scan_resident(c, c->d_data, n, c->d_res_line, c->d_res_start, c->d_res_len, c->res_cap, &count)) !=
+    if ((rc = scan_resident(c, c->d_data, n, c->d_res_line, c->d_res_start, c->d_res_len, c->res_cap, count)) !=
         DGREP_OK)
       return rc;
-    if (count <= c->res_cap) break;
-    want = count;
+    if (*count <= c->res_cap) break;
+    want = *count;
   }
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_result* out) {
+  if (!c || !out || (n && !data)) return DGREP_E_INVALID;
+  memset(out, 0, sizeof *out);
+  if (!c->loaded) { c->err = "no DFA loaded"; return DGREP_E_NO_DFA; }
+  HIPCHK(hipSetDevice(c->device));
+  uint64_t count = 0;
+  int rc;
+  if ((rc = scan_host(c, data, n, &count)) != DGREP_OK) return rc;
   out->count = count;
   if (count == 0) return DGREP_OK;
   out->line_no = static_cast<uint64_t*>(malloc(count * 8));
@@ -490,6 +510,113 @@ extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_res
   HIPCHK(hipMemcpyAsync(out->start, c->d_res_start, count * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(out->len, c->d_res_len, count * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  return DGREP_OK;
+}
+
+// ---- partition + intermediate writer (map_reduce/worker.go:13-17,78-109) ----
+static int encode_resident(dgrep_ctx* c, const uint8_t* d_data, const uint64_t* d_line, const uint64_t* d_start,
+                           const uint32_t* d_len, uint64_t count, const char* filename, size_t fn, uint32_t nreduce,
+                           uint8_t* d_out, uint64_t out_cap, uint64_t* begin, uint64_t* end, uint64_t* total) {
+  if (nreduce == 0 || nreduce > 65535) { c->err = "nreduce must be 1..65535"; return DGREP_E_INVALID; }
+  if (count >= (uint64_t(1) << 32)) { c->err = "more than 2^32-1 records"; return DGREP_E_UNSUPPORTED; }
+  int rc;
+  const uint8_t* fname = reinterpret_cast<const uint8_t*>(filename);
+  const uint64_t fj = json_escape_host(fname, fn, nullptr);
+  if (fj >= (uint64_t(1) << 31)) { c->err = "filename too long"; return DGREP_E_INVALID; }
+  std::vector<uint8_t> fjson(fj + 1);
+  json_escape_host(fname, fn, fjson.data());
+  if ((rc = grow(c, &c->d_fname, &c->fname_cap, fj + 1)) != DGREP_OK) return rc;
+  HIPCHK(hipMemcpyAsync(c->d_fname, fjson.data(), fj + 1, hipMemcpyHostToDevice, c->stream));
+  if ((rc = grow(c, &c->d_bounds, &c->bounds_cap, 2 * uint64_t(nreduce) + 1)) != DGREP_OK) return rc;
+  EncodeArgs a;
+  a.data = d_data;
+  a.line_no = d_line;
+  a.start = d_start;
+  a.len = d_len;
+  a.count = count;
+  a.fname_json = c->d_fname;
+  a.fname_json_len = uint32_t(fj);
+  a.key_hash0 = key_prefix_hash(fname, fn);
+  a.nreduce = nreduce;
+  size_t need = 0;
+  HIPCHK(encode_partitions(a, nullptr, &need, nullptr, 0, nullptr, c->stream));
+  if ((rc = grow(c, &c->d_enc_scratch, &c->enc_scratch_cap, need)) != DGREP_OK) return rc;
+  size_t have = c->enc_scratch_cap;
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  HIPCHK(encode_partitions(a, c->d_enc_scratch, &have, d_out, out_cap, c->d_bounds, c->stream));
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  std::vector<uint64_t> b(2 * size_t(nreduce) + 1);
+  HIPCHK(hipMemcpyAsync(b.data(), c->d_bounds, b.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipEventElapsedTime(&c->last_encode_ms, c->ev0, c->ev1));
+  for (uint32_t p = 0; p < nreduce; ++p) {
+    begin[p] = b[p];
+    end[p] = b[nreduce + p];
+  }
+  *total = b[2 * size_t(nreduce)];
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_encode_device(dgrep_ctx* c, const void* d_data, size_t n, const uint64_t* d_line_no,
+                                   const uint64_t* d_start, const uint32_t* d_len, uint64_t count,
+                                   const char* filename, size_t fn, uint32_t nreduce, void* d_out, uint64_t out_cap,
+                                   uint64_t* part_begin, uint64_t* part_end, uint64_t* total) {
+  if (!c || !part_begin || !part_end || !total || (fn && !filename) || (count && (!d_line_no || !d_start || !d_len)) ||
+      (n && !d_data) || (out_cap && !d_out))
+    return DGREP_E_INVALID;
+  HIPCHK(hipSetDevice(c->device));
+  return encode_resident(c, static_cast<const uint8_t*>(d_data), d_line_no, d_start, d_len, count, filename, fn,
+                         nreduce, static_cast<uint8_t*>(d_out), out_cap, part_begin, part_end, total);
+}
+
+extern "C" int dgrep_map_partitions(dgrep_ctx* c, const uint8_t* data, size_t n, const char* filename, size_t fn,
+                                    uint32_t nreduce, dgrep_partitions* out) {
+  if (!c || !out || (n && !data) || (fn && !filename) || nreduce == 0) return DGREP_E_INVALID;
+  memset(out, 0, sizeof *out);
+  if (!c->loaded) { c->err = "no DFA loaded"; return DGREP_E_NO_DFA; }
+  HIPCHK(hipSetDevice(c->device));
+  uint64_t count = 0;
+  int rc;
+  if ((rc = scan_host(c, data, n, &count)) != DGREP_OK) return rc;
+  out->nreduce = nreduce;
+  out->begin = static_cast<uint64_t*>(calloc(nreduce, 8));
+  out->end = static_cast<uint64_t*>(calloc(nreduce, 8));
+  if (!out->begin || !out->end) { dgrep_partitions_free(out); return DGREP_E_NOMEM; }
+  const uint8_t* dd = c->d_data ? c->d_data : reinterpret_cast<const uint8_t*>(c->d_counters);
+  uint64_t total = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if ((rc = encode_resident(c, dd, c->d_res_line, c->d_res_start, c->d_res_len, count, filename, fn, nreduce,
+                              c->d_enc_out, c->enc_out_cap, out->begin, out->end, &total)) != DGREP_OK) {
+      dgrep_partitions_free(out);
+      return rc;
+    }
+    if (total <= c->enc_out_cap) break;
+    if ((rc = grow(c, &c->d_enc_out, &c->enc_out_cap, total + total / 16)) != DGREP_OK) {
+      dgrep_partitions_free(out);
+      return rc;
+    }
+  }
+  out->total = total;
+  if (total) {
+    out->bytes = static_cast<uint8_t*>(malloc(total));
+    if (!out->bytes) { dgrep_partitions_free(out); return DGREP_E_NOMEM; }
+    HIPCHK(hipMemcpyAsync(out->bytes, c->d_enc_out, total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  return DGREP_OK;
+}
+
+extern "C" void dgrep_partitions_free(dgrep_partitions* p) {
+  if (!p) return;
+  free(p->begin);
+  free(p->end);
+  free(p->bytes);
+  memset(p, 0, sizeof *p);
+}
+
+extern "C" int dgrep_last_encode_ms(dgrep_ctx* c, float* ms) {
+  if (!c || !ms) return DGREP_E_INVALID;
+  *ms = c->last_encode_ms;
   return DGREP_OK;
 }
 

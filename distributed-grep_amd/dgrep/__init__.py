@@ -52,6 +52,7 @@ EXPORTS = (
     "dgrep_last_error", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
     "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_ingest", "dgrep_last_ingest_ms",
+    "dgrep_map_partitions", "dgrep_partitions_free", "dgrep_encode_device", "dgrep_last_encode_ms",
 )
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
@@ -70,6 +71,11 @@ class UnsupportedPattern(DgrepError):
 class _Result(ctypes.Structure):
     _fields_ = [("count", ctypes.c_uint64), ("line_no", ctypes.POINTER(ctypes.c_uint64)),
                 ("start", ctypes.POINTER(ctypes.c_uint64)), ("len", ctypes.POINTER(ctypes.c_uint32))]
+
+
+class _Partitions(ctypes.Structure):
+    _fields_ = [("nreduce", ctypes.c_uint32), ("total", ctypes.c_uint64), ("begin", ctypes.POINTER(ctypes.c_uint64)),
+                ("end", ctypes.POINTER(ctypes.c_uint64)), ("bytes", ctypes.c_void_p)]
 
 
 class _BlobInfo(ctypes.Structure):
@@ -126,6 +132,16 @@ def lib() -> ctypes.CDLL:
             L.dgrep_set_ingest.restype = i
             L.dgrep_last_ingest_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
             L.dgrep_last_ingest_ms.restype = i
+            L.dgrep_map_partitions.argtypes = [vp, vp, sz, ctypes.c_char_p, sz, ctypes.c_uint32,
+                                               ctypes.POINTER(_Partitions)]
+            L.dgrep_map_partitions.restype = i
+            L.dgrep_partitions_free.argtypes = [ctypes.POINTER(_Partitions)]
+            L.dgrep_partitions_free.restype = None
+            L.dgrep_encode_device.argtypes = [vp, vp, sz, vp, vp, vp, u64, ctypes.c_char_p, sz, ctypes.c_uint32, vp,
+                                              u64, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
+            L.dgrep_encode_device.restype = i
+            L.dgrep_last_encode_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+            L.dgrep_last_encode_ms.restype = i
             _lib = L
     return _lib
 
@@ -259,6 +275,40 @@ class Context:
     def last_ingest_ms(self) -> float:
         ms = ctypes.c_float()
         self._check(self._L.dgrep_last_ingest_ms(self._h, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def map_partitions(self, filename, contents, nreduce: int) -> List[bytes]:
+        """Map + writeMapOutput of one split on the GPU (dgrep_map_partitions):
+        element p is the byte content of mr-<task>-<p> (map_reduce/worker.go:78-109)."""
+        if isinstance(contents, str):
+            contents = contents.encode("utf-8", "surrogateescape")
+        fname = filename.encode("utf-8", "surrogateescape") if isinstance(filename, str) else bytes(filename)
+        buf = np.frombuffer(contents, dtype=np.uint8) if len(contents) else np.zeros(1, np.uint8)
+        res = _Partitions()
+        self._check(self._L.dgrep_map_partitions(self._h, ctypes.c_void_p(buf.ctypes.data), len(contents), fname,
+                                                 len(fname), nreduce, ctypes.byref(res)))
+        try:
+            raw = ctypes.string_at(res.bytes, res.total) if res.total else b""
+            return [raw[res.begin[p]:res.end[p]] for p in range(nreduce)]
+        finally:
+            self._L.dgrep_partitions_free(ctypes.byref(res))
+
+    def encode_device(self, d_data: int, n: int, d_line: int, d_start: int, d_len: int, count: int, filename,
+                      nreduce: int, d_out: int, out_cap: int):
+        """dgrep_encode_device: returns (begin[], end[], total)."""
+        fname = filename.encode("utf-8", "surrogateescape") if isinstance(filename, str) else bytes(filename)
+        b = (ctypes.c_uint64 * nreduce)()
+        e = (ctypes.c_uint64 * nreduce)()
+        tot = ctypes.c_uint64()
+        self._check(self._L.dgrep_encode_device(self._h, ctypes.c_void_p(d_data), n, ctypes.c_void_p(d_line),
+                                                ctypes.c_void_p(d_start), ctypes.c_void_p(d_len), count, fname,
+                                                len(fname), nreduce, ctypes.c_void_p(d_out), out_cap, b, e,
+                                                ctypes.byref(tot)))
+        return list(b), list(e), int(tot.value)
+
+    def last_encode_ms(self) -> float:
+        ms = ctypes.c_float()
+        self._check(self._L.dgrep_last_encode_ms(self._h, ctypes.byref(ms)))
         return float(ms.value)
 
     def last_kernel_ms(self) -> float:

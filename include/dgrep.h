@@ -113,6 +113,38 @@ int dgrep_set_ingest(dgrep_ctx* ctx, size_t chunk_bytes, int nbufs, int threads)
 int dgrep_last_ingest_ms(dgrep_ctx* ctx, float* ms);
 void dgrep_result_free(dgrep_result* r);
 
+/* ---- partition + intermediate writer (map_reduce/worker.go:13-17,78-109) ---
+ * The worker's writeMapOutput over one split's Map output, on the GPU: each
+ * matching line's KeyValue{Key: Sprintf("%s (line number #%v)", filename,
+ * line_no), Value: line} (application/grep.go:25-28) goes to partition
+ * ihash(Key) % nreduce (FNV-1a 32 & 0x7fffffff, worker.go:13-17) as the line
+ * json.NewEncoder(f).Encode(&kv) writes ({"Key":...,"Value":...}\n, HTML
+ * escaping on, invalid UTF-8 as \ufffd, worker.go:92-93), in Map output
+ * (line) order inside each partition. Partition p's bytes are
+ * bytes[begin[p]:end[p]] -- exactly the content of mr-<task>-<p>. */
+typedef struct {
+  uint32_t nreduce;
+  uint64_t total;   /* bytes over all partitions */
+  uint64_t* begin;  /* nreduce byte offsets into bytes */
+  uint64_t* end;
+  uint8_t* bytes;
+} dgrep_partitions;
+
+/* Host split -> ingest -> scan -> encode -> host partitions (the Map +
+ * writeMapOutput of one map task). */
+int dgrep_map_partitions(dgrep_ctx* ctx, const uint8_t* data, size_t n, const char* filename, size_t fn,
+                         uint32_t nreduce, dgrep_partitions* out);
+void dgrep_partitions_free(dgrep_partitions* p);
+/* Device form over dgrep_scan_device's records: writes into d_out (out_cap
+ * bytes; *total receives the bytes needed -- if larger, call again with a
+ * bigger buffer); part_begin/part_end are host arrays of nreduce entries. */
+int dgrep_encode_device(dgrep_ctx* ctx, const void* d_data, size_t n, const uint64_t* d_line_no,
+                        const uint64_t* d_start, const uint32_t* d_len, uint64_t count, const char* filename,
+                        size_t fn, uint32_t nreduce, void* d_out, uint64_t out_cap, uint64_t* part_begin,
+                        uint64_t* part_end, uint64_t* total);
+/* Device time (ms) of the last encode (HIP events on the context stream). */
+int dgrep_last_encode_ms(dgrep_ctx* ctx, float* ms);
+
 /* HBM-resident split (the data never leaves the device): results are written
  * to caller-provided device arrays of `capacity` entries; *count receives
  * the number of matching lines (if > capacity, nothing beyond capacity is
