@@ -74,6 +74,9 @@ constexpr uint32_t kWideClassBytes = 256;
 #define DGREP_WIDE_HOT_KIB 96
 #endif
 constexpr uint32_t kWideHotBytes = DGREP_WIDE_HOT_KIB * 1024;
-constexpr int kWideThreads = 1024;  // one workgroup per CU shares one LDS copy
+#ifndef DGREP_WIDE_THREADS
+#define DGREP_WIDE_THREADS 1024
+#endif
+constexpr int kWideThreads = DGREP_WIDE_THREADS;  // one workgroup per CU shares one LDS copy
 
 }  // namespace dgrep

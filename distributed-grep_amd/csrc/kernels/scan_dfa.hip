@@ -108,6 +108,16 @@
 #ifndef DGREP_WIDE_BLOCK
 #define DGREP_WIDE_BLOCK 64
 #endif
+// non-temporal split loads per stepper (see load_block)
+#ifndef DGREP_NT_WIDE
+#define DGREP_NT_WIDE 0
+#endif
+#ifndef DGREP_NT_TABLE
+#define DGREP_NT_TABLE 0
+#endif
+#ifndef DGREP_NT_SHENG
+#define DGREP_NT_SHENG 0
+#endif
 #ifndef DGREP_SHENG_SCHED_BARRIER
 #define DGREP_SHENG_SCHED_BARRIER 0
 #endif
@@ -496,11 +506,26 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   blk_finish(b, s, r);
 }
 
-template <int BK>
+// Split loads. NT: non-temporal (streaming) loads, so the once-read split does
+// not evict what must stay in L2 (the wide stepper's cold table rows).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int BK, bool NT = false>
 __device__ __forceinline__ void load_block(uint4 (&v)[BK / 16], const uint8_t* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-  for (int i = 0; i < BK / 16; ++i) v[i] = q[i];
+  for (int i = 0; i < BK / 16; ++i) {
+    if constexpr (NT) {
+      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q) + i);
+      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+    } else {
+      v[i] = q[i];
+    }
+  }
+}
+template <class Step>
+constexpr bool nt_loads() {
+  return (Step::kKind == kStepWide && DGREP_NT_WIDE) || (Step::kKind == kStepTable && DGREP_NT_TABLE) ||
+         (Step::kKind == kStepSheng8 && DGREP_NT_SHENG);
 }
 
 // The last < BLOCK bytes of the split, one byte at a time, then the end of the
@@ -556,19 +581,19 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   bool snap = false;
   uint64_t pos = pos0;
   uint4 A[BK / 16], B[BK / 16];
-  if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
+  if (pos0 + BK <= avail) load_block<BK, nt_loads<Step>()>(A, p + pos0);
   for (;;) {
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
     if (pos + BK > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
-    load_block<BK>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
+    load_block<BK, nt_loads<Step>()>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
     run_block<BK>(st, M, A, pos, uint64_t(C), r, emit);
     pos += BK;
 
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
     if (pos + BK > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
-    load_block<BK>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
+    load_block<BK, nt_loads<Step>()>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
     run_block<BK>(st, M, B, pos, uint64_t(C), r, emit);
     pos += BK;
   }
@@ -598,15 +623,15 @@ __device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uin
   const uint8_t* pa = a.data + csa;
   const uint8_t* pb = a.data + csb;
   uint4 A0[BK / 16], A1[BK / 16], B0[BK / 16], B1[BK / 16];
-  load_block<BK>(A0, pa);
-  load_block<BK>(B0, pb);
+  load_block<BK, nt_loads<Step>()>(A0, pa);
+  load_block<BK, nt_loads<Step>()>(B0, pb);
   for (uint32_t pos = 0; pos < uint32_t(C); pos += 2 * BK) {
-    load_block<BK>(A1, pa + pos + BK);
-    load_block<BK>(B1, pb + pos + BK);
+    load_block<BK, nt_loads<Step>()>(A1, pa + pos + BK);
+    load_block<BK, nt_loads<Step>()>(B1, pb + pos + BK);
     run_block2<BK>(st, M, A0, B0, pos, uint64_t(C), ra, rb, ea, eb);
     if (pos + 2 * BK < uint32_t(C)) {
-      load_block<BK>(A0, pa + pos + 2 * BK);
-      load_block<BK>(B0, pb + pos + 2 * BK);
+      load_block<BK, nt_loads<Step>()>(A0, pa + pos + 2 * BK);
+      load_block<BK, nt_loads<Step>()>(B0, pb + pos + 2 * BK);
     }
     run_block2<BK>(st, M, A1, B1, pos + BK, uint64_t(C), ra, rb, ea, eb);
   }
@@ -719,7 +744,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // waves per SIMD the register allocation must leave room for
 template <class Step>
 constexpr int waves_per_simd() {
-  return Step::kKind == kStepSheng8 ? DGREP_SHENG_WAVES : Step::kKind == kStepTable ? DGREP_TABLE_WAVES : 4;
+  return Step::kKind == kStepSheng8 ? DGREP_SHENG_WAVES : Step::kKind == kStepTable ? DGREP_TABLE_WAVES : kWideThreads / 256;
 }
 
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
