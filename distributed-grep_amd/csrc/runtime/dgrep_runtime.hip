@@ -18,6 +18,7 @@
 #include "../../../include/dgrep.h"
 #include "../../../include/dgrep_blob.h"
 #include "../kernels/encode.h"
+#include "../kernels/reduce.h"
 #include "../kernels/scan_common.h"
 #include "../kernels/synth.h"
 
@@ -111,6 +112,12 @@ struct dgrep_ctx {
   uint8_t* d_enc_out = nullptr;
   uint64_t enc_out_cap = 0;
   float last_encode_ms = 0.f;
+
+  // reduce task (dgrep_reduce)
+  uint8_t* d_red_scratch = nullptr;
+  uint64_t red_scratch_cap = 0;
+  uint8_t* d_red_out = nullptr;
+  uint64_t red_out_cap = 0;
 };
 
 namespace {
@@ -166,7 +173,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_table, c->d_wide, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
-                  c->d_fname, c->d_bounds, c->d_enc_out};
+                  c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -612,6 +619,63 @@ extern "C" void dgrep_partitions_free(dgrep_partitions* p) {
   free(p->end);
   free(p->bytes);
   memset(p, 0, sizeof *p);
+}
+
+// ---- reduce task (map_reduce/worker.go:22-68,161-165 + grep.go:38-40) -------
+extern "C" int dgrep_reduce(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_reduce_out* out) {
+  if (!c || !out || (n && !data)) return DGREP_E_INVALID;
+  memset(out, 0, sizeof *out);
+  HIPCHK(hipSetDevice(c->device));
+  if (n == 0) return DGREP_OK;
+  int rc;
+  uint64_t cap = c->data_cap;
+  if ((rc = grow(c, &c->d_data, &cap, (n + 63) & ~uint64_t(63))) != DGREP_OK) return rc;
+  c->data_cap = cap;
+  if ((rc = ingest(c, data, n)) != DGREP_OK) return rc;
+  uint64_t* d_info = reinterpret_cast<uint64_t*>(c->d_counters);  // 3 of its 4 u64
+  HIPCHK(reduce_count_lines(c->d_data, n, d_info, c->stream));
+  uint64_t nlines = 0;
+  HIPCHK(hipMemcpyAsync(&nlines, d_info, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (data[n - 1] != '\n') {
+    c->err = "reduce input must be whole json.Encoder lines (the last byte is not '\\n')";
+    return DGREP_E_INVALID;
+  }
+  size_t need = 0;
+  HIPCHK(reduce_lines(c->d_data, n, nlines, nullptr, &need, nullptr, 0, d_info, c->stream));
+  if ((rc = grow(c, &c->d_red_scratch, &c->red_scratch_cap, need)) != DGREP_OK) return rc;
+  uint64_t info[3] = {0, 0, 0};
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    size_t have = c->red_scratch_cap;
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    HIPCHK(reduce_lines(c->d_data, n, nlines, c->d_red_scratch, &have, c->d_red_out, c->red_out_cap, d_info,
+                        c->stream));
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    HIPCHK(hipMemcpyAsync(info, d_info, sizeof info, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (info[1] != UINT64_MAX) {
+      c->err = "reduce input line " + std::to_string(info[1] + 1) + " is not a json.Encoder KeyValue line";
+      return DGREP_E_INVALID;
+    }
+    if (info[2] <= c->red_out_cap) break;
+    if ((rc = grow(c, &c->d_red_out, &c->red_out_cap, info[2])) != DGREP_OK) return rc;
+  }
+  HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  out->lines_in = info[0];
+  out->total = info[2];
+  if (info[2]) {
+    out->bytes = static_cast<uint8_t*>(malloc(info[2]));
+    if (!out->bytes) return DGREP_E_NOMEM;
+    HIPCHK(hipMemcpyAsync(out->bytes, c->d_red_out, info[2], hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  return DGREP_OK;
+}
+
+extern "C" void dgrep_reduce_free(dgrep_reduce_out* r) {
+  if (!r) return;
+  free(r->bytes);
+  memset(r, 0, sizeof *r);
 }
 
 extern "C" int dgrep_last_encode_ms(dgrep_ctx* c, float* ms) {

@@ -53,6 +53,7 @@ EXPORTS = (
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
     "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_ingest", "dgrep_last_ingest_ms",
     "dgrep_map_partitions", "dgrep_partitions_free", "dgrep_encode_device", "dgrep_last_encode_ms",
+    "dgrep_reduce", "dgrep_reduce_free",
 )
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
@@ -76,6 +77,10 @@ class _Result(ctypes.Structure):
 class _Partitions(ctypes.Structure):
     _fields_ = [("nreduce", ctypes.c_uint32), ("total", ctypes.c_uint64), ("begin", ctypes.POINTER(ctypes.c_uint64)),
                 ("end", ctypes.POINTER(ctypes.c_uint64)), ("bytes", ctypes.c_void_p)]
+
+
+class _ReduceOut(ctypes.Structure):
+    _fields_ = [("lines_in", ctypes.c_uint64), ("total", ctypes.c_uint64), ("bytes", ctypes.c_void_p)]
 
 
 class _BlobInfo(ctypes.Structure):
@@ -142,6 +147,10 @@ def lib() -> ctypes.CDLL:
             L.dgrep_encode_device.restype = i
             L.dgrep_last_encode_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
             L.dgrep_last_encode_ms.restype = i
+            L.dgrep_reduce.argtypes = [vp, vp, sz, ctypes.POINTER(_ReduceOut)]
+            L.dgrep_reduce.restype = i
+            L.dgrep_reduce_free.argtypes = [ctypes.POINTER(_ReduceOut)]
+            L.dgrep_reduce_free.restype = None
             _lib = L
     return _lib
 
@@ -305,6 +314,17 @@ class Context:
                                                 len(fname), nreduce, ctypes.c_void_p(d_out), out_cap, b, e,
                                                 ctypes.byref(tot)))
         return list(b), list(e), int(tot.value)
+
+    def reduce(self, data: bytes) -> bytes:
+        """One grep reduce task on the GPU (dgrep_reduce): data = the
+        concatenated mr-<map>-<r> files; returns the content of mr-out-<r>."""
+        buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+        res = _ReduceOut()
+        self._check(self._L.dgrep_reduce(self._h, ctypes.c_void_p(buf.ctypes.data), len(data), ctypes.byref(res)))
+        try:
+            return ctypes.string_at(res.bytes, res.total) if res.total else b""
+        finally:
+            self._L.dgrep_reduce_free(ctypes.byref(res))
 
     def last_encode_ms(self) -> float:
         ms = ctypes.c_float()

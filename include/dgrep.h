@@ -145,6 +145,23 @@ int dgrep_encode_device(dgrep_ctx* ctx, const void* d_data, size_t n, const uint
 /* Device time (ms) of the last encode (HIP events on the context stream). */
 int dgrep_last_encode_ms(dgrep_ctx* ctx, float* ms);
 
+/* ---- reduce task (map_reduce/worker.go:22-68,161-165; grep.go:38-40) ------
+ * One reduce task of the grep job on the GPU: `data` = the concatenated
+ * mr-<map>-<r> files of partition r (json.Encoder KeyValue lines, as
+ * readReduceInput decodes them); the result is one "key value\n" line
+ * (fmt "%v %v\n" of the raw strings) per distinct key with one of its values
+ * (the grep Reduce returns values[0] after an unstable sort, so any value of
+ * a duplicated key is a valid result), in input order of the kept lines (the
+ * reference writes them in Go map order, i.e. unordered). A line that is not a
+ * json.Encoder KeyValue line fails with DGREP_E_INVALID (never guessed). */
+typedef struct {
+  uint64_t lines_in; /* KeyValue lines read */
+  uint64_t total;    /* output bytes */
+  uint8_t* bytes;    /* the content of mr-out-<r> */
+} dgrep_reduce_out;
+int dgrep_reduce(dgrep_ctx* ctx, const uint8_t* data, size_t n, dgrep_reduce_out* out);
+void dgrep_reduce_free(dgrep_reduce_out* r);
+
 /* HBM-resident split (the data never leaves the device): results are written
  * to caller-provided device arrays of `capacity` entries; *count receives
  * the number of matching lines (if > capacity, nothing beyond capacity is

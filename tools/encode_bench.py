@@ -1,6 +1,7 @@
 """Throughput of the GPU partition + intermediate writer (dgrep_encode_device)
 over the Map output of an HBM-resident split, next to
-the oracle's CPU restatement of writeMapOutput on a sample. Run on the GPU box:
+the oracle's CPU restatement of writeMapOutput on a sample, then the reduce
+(dgrep_reduce) over all the encoded lines. Run on the GPU box:
 
     python tools/encode_bench.py [--workload c2] [--gib 16] [--nreduce 10]
 
@@ -69,13 +70,21 @@ def main():
     for p in range(args.nreduce):
         assert raw[b[p]:b[p] + len(parts[p])] == bytes(parts[p]), p
     best = min(ms)
+    # the reduce side: every partition's lines through dgrep_reduce (all keys distinct)
+    red_ms, red_out = [], b""
+    for _ in range(3):
+        red_out = ctx.reduce(raw[: total])
+        red_ms.append(ctx.last_kernel_ms())
+    assert red_out.count(b"\n") == cnt
     print(json.dumps({
         "what": "GPU partition + intermediate writer (ihash %% nReduce, json.Encoder lines), map_reduce/worker.go:78-109",
         "workload": wl["desc"], "records": cnt, "nreduce": args.nreduce, "value_bytes": value_bytes,
         "output_bytes": total, "encode_ms_best": round(best, 3), "encode_ms_all": [round(x, 3) for x in ms],
         "records_per_s": round(cnt / (best * 1e-3)), "output_gbs": round(total / (best * 1e-3) / 1e9, 2),
         "cpu_oracle_records_per_s_1core": round(2000 / cpu_s),
-        "checked": "first 2,000 records bit-exact vs oracle per partition prefix"}), flush=True)
+        "checked": "first 2,000 records bit-exact vs oracle per partition prefix",
+        "reduce_ms_best": round(min(red_ms), 3), "reduce_lines_per_s": round(cnt / (min(red_ms) * 1e-3)),
+        "reduce_output_bytes": len(red_out)}), flush=True)
     ctx.close()
 
 
