@@ -46,6 +46,35 @@ def test_oracle_ihash_pinned():
     assert O.format_key(b"f.log", 12) == b"f.log (line number #12)"
 
 
+def _go_json_str_witness(b: bytes) -> bytes:
+    """Go encoding/json string encoding (HTML escaping on) derived from Python's
+    json module for VALID UTF-8: Python leaves <>& and U+2028/9 alone and uses
+    \\b \\f short forms, Go 1.18 does not."""
+    import json as J
+
+    s = J.dumps(b.decode("utf-8"), ensure_ascii=False)
+    s = s.replace("\\b", "\\u0008").replace("\\f", "\\u000c")
+    s = s.replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+    s = s.replace("\u2028", "\\u2028").replace("\u2029", "\\u2029")
+    return s.encode("utf-8")
+
+
+def test_oracle_json_kv_vs_python_json():
+    """The oracle's json.Encoder restatement against an independent witness on
+    valid UTF-8 (invalid UTF-8 -> \\ufffd per byte stays pinned only by the
+    restatement of utf8.DecodeRune)."""
+    import random
+
+    rnd = random.Random(5)
+    pool = ["a", "Z", " ", "<", ">", "&", '"', "\\", "/", "\n", "\r", "\t", "\b", "\f", "\x00", "\x1f", "\x7f",
+            "é", "€", "\u2028", "\u2029", "\U0001F600", "#", "(", ")"]
+    for _ in range(400):
+        k = "".join(rnd.choice(pool) for _ in range(rnd.randrange(0, 12))).encode()
+        v = "".join(rnd.choice(pool) for _ in range(rnd.randrange(0, 40))).encode()
+        want = b'{"Key":' + _go_json_str_witness(k) + b',"Value":' + _go_json_str_witness(v) + b"}\n"
+        assert O.json_kv(k, v) == want, (k, v)
+
+
 def expected_partitions(pattern: bytes, filename: bytes, data: bytes, nreduce: int):
     ln, st, le = O.grep_map(pattern, data, threads=16)
     parts = [bytearray() for _ in range(nreduce)]
