@@ -156,9 +156,10 @@ def main():
         verified = verify_windows(buf, n, line_t[:count], start_t[:count], len_t[:count], pattern,
                                   args.verify_windows, wl.get("verify_window", 2 << 20))
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(buf, n, pattern, args.cpu_seconds)
+        cpu_mt = cpu_baseline_mt(buf, n, pattern, args.cpu_seconds / 2)
 
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
@@ -210,6 +211,7 @@ def main():
                 "algorithmic_bytes_per_launch": int(n + STAGED_LINE_BYTES * count),
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_mt": cpu_mt,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -309,6 +311,50 @@ def cpu_baseline(buf, n, pattern, seconds):
         "kind": "port",
         "sample": "first %.2f MiB of the same split (%d matching lines), oracle/ grep.go Map restatement with "
                   "per-line pattern compile (as grep.go:21), 1 thread, %.1f s" % (done / 2**20, matches, dt),
+    }
+
+
+def cpu_baseline_mt(buf, n, pattern, seconds):
+    """SURVEY.md §8d comparator (3): the oracle's Map with the pattern compiled
+    once per call, lines split over T host threads (T = the box's CPU share,
+    at most 16). Bounded like cpu_baseline: doubling whole-line pieces from the
+    split's start (256 KiB up to 64 MiB, sized to the time left) until `seconds` of wall time are spent."""
+    import ctypes
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    T = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)))
+    L = O.lib()
+    pat = pattern.encode()
+    piece, done, matches, dt = 256 << 10, 0, 0, 0.0
+    while dt < seconds and done < n:
+        data = buf[done:min(n, done + piece)].cpu().numpy()
+        nl = np.flatnonzero(data == 10)
+        data = data[: int(nl[-1]) + 1] if nl.size else data
+        cap = int(nl.size) + 1
+        ln = np.zeros(cap, np.uint64)
+        st = np.zeros(cap, np.uint64)
+        le = np.zeros(cap, np.uint32)
+        t = time.perf_counter()
+        cnt = L.orc_map_mt(pat, len(pat), data.ctypes.data, len(data), T, ln.ctypes.data, st.ctypes.data,
+                           le.ctypes.data, cap)
+        dt += time.perf_counter() - t
+        if cnt < 0 or cnt > cap:
+            return None
+        done += len(data)
+        matches += int(cnt)
+        # next piece: double, but no more than the remaining time allows
+        piece = int(max(64 << 10, min(piece * 2, 64 << 20, done / dt * (seconds - dt))))
+    return {
+        "value": round(done / dt / 1e9, 6),
+        "unit": "GB/s",
+        "cores": T,
+        "kind": "port",
+        "sample": "first %.2f MiB of the same split (%d matching lines), oracle/ Map restatement with the pattern "
+                  "compiled once per call, lines split over %d threads, %.1f s" % (done / 2**20, matches, T, dt),
     }
 
 

@@ -193,6 +193,11 @@ struct StepSheng8 {
   }
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[b], s); }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return (s & 0xffu) == M; }
+  // states are replicated bytes and start_m is the highest state (host
+  // renumbering): one max over the word's four states replaces four compares
+  __device__ __forceinline__ static bool any4(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t M) {
+    return max(max(s0, s1), max(s2, s3)) >= M * 0x01010101u;
+  }
   // map <- transitions of bytes 0..lim of the word applied to the 8-state map
   // (lo: states 0-3, hi: states 4-7); one v_perm per byte and half
   __device__ __forceinline__ void compose(const Pre& p, uint32_t lim, uint32_t& lo, uint32_t& hi) const {
@@ -384,7 +389,12 @@ template <int J, bool TRACK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
                                             uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
-  if (__builtin_expect(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)), 0)) {
+  bool any;
+  if constexpr (Step::kKind == kStepSheng8)
+    any = StepSheng8::any4(s0, s1, s2, s3, M);
+  else
+    any = bool(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)));
+  if (__builtin_expect(any, 0)) {
     // a '\n' in this word ends a matching line: resolve it exactly
     const uint64_t q0 = b.pos + 4u * J;
     const bool seen_w = r.seen || b.lastm != 0;

@@ -257,9 +257,20 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   } else if (h.nstates <= DGREP_SHENG_MAX_STATES) {
     // StepSheng8: V[b] = 8 bytes, byte s = next state of s on input byte b
     c->step_kind = kStepSheng8;
+    // renumber so start_m is the highest state (the kernel tests a word's four
+    // states for start_m with one max), and carry the start state replicated
+    // in all four bytes: v_perm keeps a replicated selector replicated, so
+    // every state on the chain is a clean 0x01010101 multiple
+    const uint32_t S = h.nstates, top = S - 1;
+    std::vector<uint32_t> id(S);
+    for (uint32_t x = 0; x < S; ++x) id[x] = x;
+    std::swap(id[h.start_m], id[top]);
     t.assign(256 * 8, 0);
     for (int b = 0; b < 256; ++b)
-      for (uint32_t s = 0; s < h.nstates; ++s) t[size_t(b) * 8 + s] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
+      for (uint32_t s = 0; s < S; ++s)
+        t[size_t(b) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
+    start = id[h.start] * 0x01010101u;
+    start_m = top;
   } else {
     // StepTable: row s (stride scan_table_row() = 260, bank-staggered) holds
     // trans[s][class(b)] at byte b
