@@ -68,6 +68,7 @@ def parse():
                     help="CPU baseline budget: whole 1 MiB pieces of the split until this much time is spent")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-windows", type=int, default=6)
+    ap.add_argument("--lane-chunk", type=int, default=0, help="tuning: force the Sheng lane chunk (0 = adaptive)")
     return ap.parse_args()
 
 
@@ -94,6 +95,8 @@ def main():
     pattern = workload_pattern(wl)
 
     ctx = dgrep.Context(local)
+    if args.lane_chunk:
+        ctx.set_lane_chunk(args.lane_chunk)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     cp = ctx.load(pattern)

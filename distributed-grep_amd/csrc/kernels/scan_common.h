@@ -36,7 +36,7 @@ struct ScanArgs {
   const uint8_t* table;   // u8 transition table, [state][byte] (nstates*256 bytes)
   uint32_t table_bytes;
   uint32_t start, start_m;
-  uint32_t pad;
+  uint32_t chunk;         // lane chunk bytes of the adaptive (Sheng) stepper, from scan_tile_bytes
   uint64_t ntiles;
   StagedLine* staging;
   uint64_t capacity;      // staging/output capacity in lines

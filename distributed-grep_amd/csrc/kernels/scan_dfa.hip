@@ -38,6 +38,8 @@
 //     the tiles out in split order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "scan_common.h"
 
 // build-time tuning knobs, per stepper (defaults are the shipped
@@ -576,9 +578,9 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
 // BK-byte blocks with direct per-lane loads, prefetching the next block while
 // the current one is stepped (two register buffers, ping-pong). Returns the
 // number of '\n' inside the lane's own chunk [cs, cs + C).
-template <int C, int BK, class Step, int E, bool DIRECT>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step& st, uint64_t cs, uint64_t pos0,
-                                                  LaneRun& r, const Emitter<E, DIRECT>& emit) {
+                                                  LaneRun& r, const Emitter<E, DIRECT>& emit, const uint32_t C) {
   const uint32_t M = a.start_m;
   const uint64_t avail = cs < a.n ? a.n - cs : 0;
   if (avail <= pos0) {
@@ -611,12 +613,12 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   return nl_chunk;
 }
 
-template <int C, int BK, class Step, int E, bool DIRECT>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
-                                             const Emitter<E, DIRECT>& emit) {
+                                             const Emitter<E, DIRECT>& emit, const uint32_t C) {
   lane_init(a, cs, r);
   if (cs >= a.n) return 0;
-  return run_lane_from<C, BK>(a, st, cs, 0, r, emit);
+  return run_lane_from<BK>(a, st, cs, 0, r, emit, C);
 }
 
 // Two chunks per lane (csa, csb), both wholly inside the split, stepped in
@@ -647,8 +649,8 @@ __device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uin
   }
   nla = ra.nl;
   nlb = rb.nl;
-  run_lane_from<C, BK>(a, st, csa, uint64_t(C), ra, ea);
-  run_lane_from<C, BK>(a, st, csb, uint64_t(C), rb, eb);
+  run_lane_from<BK>(a, st, csa, uint64_t(C), ra, ea, uint32_t(C));
+  run_lane_from<BK>(a, st, csb, uint64_t(C), rb, eb, uint32_t(C));
 }
 
 // 16 bytes global -> LDS (global_load_lds_dwordx4); the LDS destination is
@@ -729,7 +731,7 @@ __device__ __forceinline__ uint32_t run_lane_staged(const ScanArgs& a, const Ste
         emit(r, uint64_t(C) + uint64_t(np1), r.prev_nl + 1, r.nl);
     }
   }
-  if (tail) run_lane_from<C, 64>(a, st, cs, uint64_t(C), r, emit);
+  if (tail) run_lane_from<64>(a, st, cs, uint64_t(C), r, emit, uint32_t(C));
   return nl_chunk;
 }
 
@@ -739,6 +741,20 @@ template <class Step, int TBL>
 constexpr bool use_staging() {
   return (DGREP_SHENG_STAGING && Step::kKind == kStepSheng8) ||
          (DGREP_TABLE_STAGING && Step::kKind == kStepTable && TBL <= 32 * int(kRow));
+}
+
+// The Sheng stepper's lane chunk is chosen per split on the host
+// (adaptive_chunk_bytes): the fixed chunks of the other steppers leave the
+// last round of tiles over the resident waves part-empty, which at 16-KiB
+// chunks costs up to a sixth of a 16-GiB split's time.
+template <class Step, int TBL>
+constexpr bool adaptive_chunk() {
+  return Step::kKind == kStepSheng8 && !use_staging<Step, TBL>();
+}
+template <class Step, int TBL>
+__device__ __forceinline__ uint32_t lane_chunk(const ScanArgs& a) {
+  if constexpr (adaptive_chunk<Step, TBL>()) return a.chunk;
+  return uint32_t(Tune<Step>::C);
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -763,8 +779,9 @@ constexpr int waves_per_simd() {
 
 template <class Step, int TBL, int NT>
 __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(ScanArgs a) {
-  constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
+  constexpr int E = Tune<Step>::E, BK = Tune<Step>::B;
   constexpr bool kStaged = use_staging<Step, TBL>();
+  const uint32_t C = lane_chunk<Step, TBL>(a);
   constexpr int R = DGREP_STAGE_ROUND;
   __shared__ ScanSmem<TBL, E * streams_of<Step, TBL>(), NT> sm;
   // the staging rings are a __shared__ object of their own: with the table in
@@ -781,7 +798,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   uint32_t* slots = sm.slots + tid * S * E * 2;
   const int lane = tid & 63;
   const uint64_t waves = uint64_t(gridDim.x) * (NT / 64);
-  constexpr uint64_t kTile = uint64_t(kTileLanes) * uint64_t(S) * uint64_t(C);
+  const uint64_t kTile = uint64_t(kTileLanes) * uint64_t(S) * uint64_t(C);
   for (uint64_t t = uint64_t(blockIdx.x) * (NT / 64) + uint64_t(tid >> 6); t < a.ntiles; t += waves) {
     uint64_t cs[S];
     LaneRun r[S];
@@ -792,21 +809,21 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
     if constexpr (S == 2) {
       const Emitter<E, false> e0{&a, slots, cs[0], 0, 0}, e1{&a, slots + E * 2, cs[1], 0, 0};
       if (full) {
-        run_lane2<C, BK>(a, st, cs[0], cs[1], r[0], r[1], e0, e1, nlc[0], nlc[1]);
+        run_lane2<Tune<Step>::C, BK>(a, st, cs[0], cs[1], r[0], r[1], e0, e1, nlc[0], nlc[1]);
       } else {
-        nlc[0] = run_lane<C, BK>(a, st, cs[0], r[0], e0);
-        nlc[1] = run_lane<C, BK>(a, st, cs[1], r[1], e1);
+        nlc[0] = run_lane<BK>(a, st, cs[0], r[0], e0, C);
+        nlc[1] = run_lane<BK>(a, st, cs[1], r[1], e1, C);
       }
     } else {
       const Emitter<E, false> em{&a, slots, cs[0], 0, 0};
       if constexpr (kStaged) {
         if (full)
-          nlc[0] = run_lane_staged<C, R>(a, st, cs[0], lane, stage + (tid >> 6) * (DGREP_STAGE_DEPTH * 64 * R), r[0],
+          nlc[0] = run_lane_staged<Tune<Step>::C, R>(a, st, cs[0], lane, stage + (tid >> 6) * (DGREP_STAGE_DEPTH * 64 * R), r[0],
                                          em);
         else
-          nlc[0] = run_lane<C, BK>(a, st, cs[0], r[0], em);
+          nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
       } else {
-        nlc[0] = run_lane<C, BK>(a, st, cs[0], r[0], em);
+        nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
       }
     }
 
@@ -871,7 +888,8 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
 // such lane runs it again in direct-write mode (rare: dense short matches).
 template <class Step, int TBL>
 __global__ __launch_bounds__(64) void scan_overflow_kernel(ScanArgs a, uint64_t nover) {
-  constexpr int C = Tune<Step>::C, E = Tune<Step>::E, BK = Tune<Step>::B;
+  constexpr int E = Tune<Step>::E, BK = Tune<Step>::B;
+  const uint32_t C = lane_chunk<Step, TBL>(a);
   __shared__ ScanSmem<TBL, 1, 64> sm;
   for (uint32_t i = threadIdx.x * 16u; i < a.table_bytes; i += 64 * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
@@ -881,7 +899,7 @@ __global__ __launch_bounds__(64) void scan_overflow_kernel(ScanArgs a, uint64_t 
     const OverflowLane ol = a.overflow[k];
     LaneRun r;
     Emitter<E, true> ed{&a, nullptr, ol.cs, ol.out_base, ol.nl_prefix};
-    run_lane<C, BK>(a, st, ol.cs, r, ed);
+    run_lane<BK>(a, st, ol.cs, r, ed, C);
   }
 }
 
@@ -1024,11 +1042,33 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (table_bytes <= 128 * kRow) return op.template run<StepTable, 128 * kRow>();
   return op.template run<StepTable, 256 * kRow>();
 }
+// Adaptive chunk: a power of two from the compiled chunk (its floor) up to
+// kShengMaxChunk, the largest that still gives every resident wave at least
+// one tile. Measured on C2 (profiles/r01/ablation/chunk_sweep.txt): 32 KiB
+// runs 5.1 TB/s, 16 KiB 4.74-4.88, 8 KiB 4.54, 4 KiB 4.29, but 14,592 B (a
+// chunk sized to fill whole rounds exactly) 4.13: keep powers of two. The LDS
+// slots pack a line's chunk-relative start (<= C) and '\n' index (<= C) in 16
+// bits each, so 32,768 is also the hard limit (65,536 fails GPU parity).
+constexpr uint64_t kShengMaxChunk = 32768;
+uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c) {
+  uint64_t c = floor_c;
+  while (c * 2 <= kShengMaxChunk && n >= waves * uint64_t(kTileLanes) * c * 2) c *= 2;
+  return uint32_t(c);
+}
 struct TileOp {
   uint64_t* bytes;
+  uint32_t* chunk;
+  uint32_t* waves_per_block;
+  uint64_t n, resident_blocks;
+  uint32_t force;
   template <class S, int T>
   hipError_t run() const {
-    *bytes = uint64_t(kTileLanes) * uint64_t(streams_of<S, T>()) * uint64_t(Tune<S>::C);
+    uint64_t c = uint64_t(Tune<S>::C);
+    if constexpr (adaptive_chunk<S, T>())
+      c = force ? uint64_t(force) : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c);
+    *chunk = uint32_t(c);
+    *waves_per_block = uint32_t(threads_of<S>() / 64);
+    *bytes = uint64_t(kTileLanes) * uint64_t(streams_of<S, T>()) * c;
     return hipSuccess;
   }
 };
@@ -1053,9 +1093,10 @@ struct OverflowOp {
 };
 }  // namespace
 
-uint64_t scan_tile_bytes(int kind, uint32_t table_bytes) {
+uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t resident_blocks, uint32_t force,
+                         uint32_t* chunk, uint32_t* waves_per_block) {
   uint64_t b = 0;
-  (void)dispatch(kind, table_bytes, TileOp{&b});
+  (void)dispatch(kind, table_bytes, TileOp{&b, chunk, waves_per_block, n, resident_blocks, force});
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {

@@ -51,7 +51,7 @@ EXPORTS = (
     "dgrep_compile", "dgrep_blob_free", "dgrep_blob_info_get", "dgrep_open", "dgrep_close",
     "dgrep_last_error", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
-    "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_ingest", "dgrep_last_ingest_ms",
+    "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_lane_chunk", "dgrep_set_ingest", "dgrep_last_ingest_ms",
     "dgrep_map_partitions", "dgrep_partitions_free", "dgrep_encode_device", "dgrep_last_encode_ms",
     "dgrep_reduce", "dgrep_reduce_free",
 )
@@ -119,6 +119,8 @@ def lib() -> ctypes.CDLL:
             L.dgrep_load_dfa.restype = i
             L.dgrep_set_stepper.argtypes = [vp, i, ctypes.c_uint32]
             L.dgrep_set_stepper.restype = i
+            L.dgrep_set_lane_chunk.argtypes = [vp, ctypes.c_uint32]
+            L.dgrep_set_lane_chunk.restype = i
             L.dgrep_scan.argtypes = [vp, vp, sz, ctypes.POINTER(_Result)]
             L.dgrep_scan.restype = i
             L.dgrep_result_free.argtypes = [ctypes.POINTER(_Result)]
@@ -234,6 +236,11 @@ class Context:
 
     def set_stream(self, hip_stream: int):
         self._check(self._L.dgrep_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
+
+    def set_lane_chunk(self, chunk_bytes: int = 0):
+        """Testing/tuning: the Sheng stepper's lane chunk for later scans
+        (dgrep_set_lane_chunk; 0 = adaptive)."""
+        self._check(self._L.dgrep_set_lane_chunk(self._h, chunk_bytes))
 
     def set_stepper(self, force_wide: bool = False, wide_hot_rows: int = 0):
         """Testing/tuning: force the wide stepper and/or cap its LDS rows for

@@ -96,6 +96,12 @@ int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
  * force_wide != 0 uses the wide (u16, LDS-hot + HBM) stepper for any DFA;
  * wide_hot_rows != 0 caps its LDS-resident rows. */
 int dgrep_set_stepper(dgrep_ctx* ctx, int force_wide, uint32_t wide_hot_rows);
+/* Tests / tuning: lane chunk of the Sheng (<= 8-state) stepper for later
+ * scans. 0 (default) = adaptive: the compiled 4 KiB chunk, doubled (up to
+ * 32 KiB) while every resident wave still gets a tile; otherwise a multiple
+ * of 128 in [4096, 32768] (LDS slots hold 16-bit chunk offsets). No effect
+ * on other steppers. */
+int dgrep_set_lane_chunk(dgrep_ctx* ctx, uint32_t chunk_bytes);
 
 /* Host bytes -> H2D -> scan -> D2H results. This is the call Map makes.
  * The H2D leg is the worker's split ingest (the bytes map_reduce/worker.go:72-76

@@ -102,6 +102,43 @@ def test_tile_and_chunk_boundaries(gpu_ctx, size):
         _check(gpu_ctx, pattern, data)
 
 
+# Sheng stepper with the lane chunks the adaptive choice produces on large
+# splits (dgrep_set_lane_chunk forces them at oracle-friendly sizes): chunk and
+# tile edges, lines longer than a chunk, and more matching lines per lane than
+# LDS slots (pattern "" matches every line: the overflow kernel)
+@pytest.mark.parametrize("chunk", [4224, 8192, 14592, 16384, 32768])
+def test_sheng_adaptive_chunks(gpu_ctx, chunk):
+    import dgrep
+
+    tile = 64 * chunk
+    try:
+        gpu_ctx.set_lane_chunk(chunk)
+        for size in (chunk - 1, chunk + 1, tile - 1, tile, tile + 1, 2 * tile + 777):
+            data = bytearray(dgrep.synth_corpus_host(size, 13, 0))
+            for edge in (chunk - 1, chunk, 2 * chunk, tile - 1, tile, tile + chunk):
+                if edge < size:
+                    data[edge] = 0x0A
+            if size > 3 * chunk:
+                data[chunk + 5:3 * chunk] = b"x" * (2 * chunk - 5)  # a line over two chunk edges
+                data[2 * chunk:2 * chunk + 5] = b"error"
+            data = bytes(data)
+            for pattern in (b"error", b"", b"^2024", b"ok$"):
+                cp = gpu_ctx.load(pattern)
+                assert cp.nstates <= 8, (pattern, cp.nstates)
+                _check(gpu_ctx, cp, data)
+    finally:
+        gpu_ctx.set_lane_chunk(0)
+
+
+def test_lane_chunk_validation(gpu_ctx):
+    import dgrep
+
+    for bad in (100, 4000, 4097, 32896, 65536, 1 << 20):
+        with pytest.raises(dgrep.DgrepError):
+            gpu_ctx.set_lane_chunk(bad)
+    gpu_ctx.set_lane_chunk(0)
+
+
 # table-stepper instantiations: <= 64 states run two chunks per lane (tile 256
 # KiB), 65-256 states one (tile 128 KiB); both at their chunk and tile edges
 @pytest.mark.parametrize("pattern", [b"(alpha|bravo|charlie|delta|echo|foxtrot|golf|hotel|india|juliet)[0-9]+",
