@@ -112,9 +112,12 @@ def vector(name: str, filename: str, pattern: bytes, data: bytes):
     keys = [O.format_key(fn, x) for x in ln]
     values = [data[s:s + n] for s, n in zip(st, le)]
     # after Reduce (grep.go:38-40 returns values[0]; keys are unique per file):
-    # one "%v %v\n" line per key (map_reduce/worker.go:111-124), compared
-    # key-sorted because the reference writes them in Go map order (worker.go:163)
-    reduce_lines = sorted(k + b" " + v + b"\n" for k, v in zip(keys, values))
+    # each KeyValue crosses the shuffle as a json.Encoder line (worker.go:92-93:
+    # an invalid UTF-8 byte becomes �) read back by json.Decoder
+    # (worker.go:53-56), then one "%v %v\n" line per key (worker.go:111-124,
+    # 163-165), compared key-sorted because the reference writes them in Go map
+    # order (worker.go:163)
+    reduce_out = O.reduce_lines(keys, values)
     return {
         "name": name,
         "filename": filename,
@@ -125,7 +128,7 @@ def vector(name: str, filename: str, pattern: bytes, data: bytes):
         "start": st,
         "len": le,
         "keys_b64": [base64.b64encode(k).decode() for k in keys],
-        "reduce_b64": base64.b64encode(b"".join(reduce_lines)).decode(),
+        "reduce_b64": base64.b64encode(reduce_out).decode(),
         "partition": [O.ihash(k) % N_REDUCE for k in keys],  # map_reduce/worker.go:13-17,84
         "witnesses": witnesses,
     }

@@ -119,3 +119,34 @@ def json_kv(key: bytes, value: bytes) -> bytes:
     out = ctypes.create_string_buffer(n)
     lib().orc_json_kv(key, len(key), value, len(value), out, n)
     return out.raw[:n]
+
+
+def _go_json_str(s: str) -> bytes:
+    # Go's json.Decoder turns a lone surrogate escape into U+FFFD; Python keeps it
+    return "".join("�" if 0xD800 <= ord(ch) < 0xE000 else ch for ch in s).encode("utf-8")
+
+
+def json_roundtrip_kv(key: bytes, value: bytes):
+    """(Key, Value) as the reduce task sees them: json.Encoder (the oracle's
+    restatement of map_reduce/worker.go:92-93, invalid UTF-8 byte -> \\ufffd)
+    then json.Decoder (worker.go:53-56). Python's json parses the encoder's
+    output (standard escapes only); the decode side maps lone surrogates to
+    U+FFFD as Go does."""
+    import json
+
+    line = json_kv(key, value)
+    assert line.endswith(b"\n"), line
+    d = json.loads(line)
+    return _go_json_str(d["Key"]), _go_json_str(d["Value"])
+
+
+def reduce_lines(keys, values) -> bytes:
+    """The grep reduce output (Reduce = values[0], grep.go:38-40) of one map
+    task's KeyValues, written "%v %v\\n" per key (map_reduce/worker.go:163-165),
+    key-sorted because the reference writes them in Go map order
+    (worker.go:163). Keys of one file are distinct."""
+    lines = []
+    for k, v in zip(keys, values):
+        k2, v2 = json_roundtrip_kv(k, v)
+        lines.append(k2 + b" " + v2 + b"\n")
+    return b"".join(sorted(lines))

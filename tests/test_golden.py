@@ -71,8 +71,43 @@ def test_keys_partitions_and_reduce_lines():
         assert keys == [base64.b64decode(k) for k in v["keys_b64"]], v["name"]
         assert [O.ihash(k) % GOLDEN["n_reduce"] for k in keys] == v["partition"], v["name"]
         vals = [d[s:s + n] for s, n in zip(v["start"], v["len"])]
-        red = b"".join(sorted(k + b" " + x + b"\n" for k, x in zip(keys, vals)))
-        assert red == base64.b64decode(v["reduce_b64"]), v["name"]
+        assert O.reduce_lines(keys, vals) == base64.b64decode(v["reduce_b64"]), v["name"]
+
+
+def test_reduce_lines_carry_the_json_roundtrip():
+    """The after-Reduce lines are what json.Encoder -> json.Decoder leave of a
+    value (map_reduce/worker.go:92-93, 53-56): every invalid UTF-8 byte is one
+    U+FFFD, so the reduce output is valid UTF-8 even where the line was not."""
+    bad = [v for v in VECTORS if any(b >= 0x80 for b in INPUTS[v["input"]]) and v["line_no"]]
+    assert bad
+    for v in VECTORS:
+        red = base64.b64decode(v["reduce_b64"])
+        red.decode("utf-8")  # strict: raises on raw invalid bytes
+    # edge12 = b"\xff\xfe\n\xe2\x82\xac\n\xe2\x82\n\xef\xbf\xbd\n": "" matches every line
+    v = next(v for v in VECTORS if v["name"] == "edge12/")
+    want = [b"f.log (line number #1) \xef\xbf\xbd\xef\xbf\xbd\n", b"f.log (line number #2) \xe2\x82\xac\n",
+            b"f.log (line number #3) \xef\xbf\xbd\xef\xbf\xbd\n", b"f.log (line number #4) \xef\xbf\xbd\n",
+            b"f.log (line number #5) \n"]
+    assert base64.b64decode(v["reduce_b64"]) == b"".join(sorted(want))
+
+
+@pytest.mark.gpu
+def test_gpu_map_partitions_reduce_reproduces_golden(gpu_ctx):
+    """End to end after Reduce, on the GPU: Map + writeMapOutput
+    (dgrep_map_partitions, nReduce 10 as main/coordinator_launch.go:17) then one
+    reduce task per partition (dgrep_reduce); the union of the mr-out-<r> lines,
+    key-sorted, must equal the vector's reduce lines."""
+    nred = GOLDEN["n_reduce"]
+    for v in VECTORS:
+        p, d = _unpack(v)
+        gpu_ctx.load(p)
+        parts = gpu_ctx.map_partitions(v["filename"], d, nred)
+        lines = []
+        for r, part in enumerate(parts):
+            out = gpu_ctx.reduce(part)
+            assert out == b"" or out.endswith(b"\n"), (v["name"], r)
+            lines += [x + b"\n" for x in out.split(b"\n")[:-1]]
+        assert b"".join(sorted(lines)) == base64.b64decode(v["reduce_b64"]), v["name"]
 
 
 @pytest.mark.gpu
