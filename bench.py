@@ -9,8 +9,10 @@ scans its own split (Map tasks shard per split, map_reduce/coordinator.go:312)
 and the compacted match records are gathered to rank 0 over xGMI in the same
 step — the only exchange the path has.
 
-Default workload (N=1): BASELINE.json configs[1] = SURVEY §8d C2: a 16 GiB
-seeded synthetic log split, literal pattern `error`, LDS-resident DFA.
+Default workload: at N=1 BASELINE.json configs[1] = SURVEY §8d C2 (a 16 GiB
+seeded synthetic log split, literal pattern `error`, LDS-resident DFA); at
+N>1 configs[4] = C5 (one 32 GiB split per GPU, seed 100 + rank, `error`, and
+the RCCL gather of the match records to rank 0 inside every step).
 `value` = whole-job GB/s of text scanned (sum over ranks / max-over-ranks
 time); `roofline` = the scan kernel's algorithmic bytes (split bytes read +
 16 B per staged match) / its HIP-event time against the 8 TB/s HBM peak;
@@ -40,6 +42,12 @@ WORKLOADS = {
     "c4": dict(pattern=None, seed=4, kind=1, gib=16.0, verify_window=256 << 10,
                desc="C4: 16 GiB split (seed 4, keywords planted), (?i) alternation of 1,000 seeded keywords, "
                     "wide DFA (hot rows in LDS, the rest in HBM/L2)"),
+    # SURVEY §8d C5 / BASELINE.json configs[4]: 8 splits x 32 GiB, seeds 100-107
+    "c5": dict(pattern="error", seed=100, rank_seed_step=1, kind=0, gib=32.0,
+               desc="C5: one 32 GiB synthetic log split per GPU (seed 100 + rank), literal 'error'"),
+    # a dense Sheng line (~60 % of lines match): the lane chunk adapts to the match density
+    "dense": dict(pattern="e", seed=2, kind=0, gib=16.0,
+                  desc="dense: 16 GiB split (seed 2), literal 'e' (most lines match)"),
 }
 
 
@@ -62,7 +70,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: c2 on one GPU, c5 on more")
     ap.add_argument("--split-gib", type=float, default=None, help="per-GPU split size (default: workload's)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU baseline budget: whole 1 MiB pieces of the split until this much time is spent")
@@ -88,6 +97,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.workload is None:
+        args.workload = "c2" if world == 1 else "c5"
     wl = WORKLOADS[args.workload]
     gib = args.split_gib if args.split_gib is not None else wl["gib"]
     n = int(gib * (1 << 30))
@@ -103,7 +114,8 @@ def main():
 
     t = time.time()
     buf = torch.empty(n + 64, dtype=torch.uint8, device=dev)
-    ctx.synth(buf.data_ptr(), n, wl["seed"] + 1000 * rank, wl["kind"])
+    seed = wl["seed"] + wl.get("rank_seed_step", 1000) * rank
+    ctx.synth(buf.data_ptr(), n, seed, wl["kind"])
     torch.cuda.synchronize(dev)
     log("rank %d: generated %.1f GiB split in %.1fs; DFA %d states x %d classes" %
         (rank, n / 2**30, time.time() - t, cp.nstates, cp.nclasses))
@@ -134,12 +146,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    kms = []
+    kms, stats = [], []
     t0 = time.perf_counter()
     count = 0
     for _ in range(args.steps):
         count = step()
-        kms.append(ctx.last_kernel_ms())
+        kms.append(ctx.last_kernel_ms())  # scan kernel + overflow pass, HIP events on the launch stream
+        stats.append(ctx.scan_stats())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -151,6 +164,8 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed / 1e9
     kern_ms = float(np.mean(kms))
+    kern_med = float(np.median(kms))
+    st = stats[-1]
     achieved = (n + STAGED_LINE_BYTES * count) / (kern_ms * 1e-3) / 1e9
 
     # ---- size-independent checks on the full split (rank 0) ----------------
@@ -201,6 +216,11 @@ def main():
                 "per_gpu_gbs": round(value / world, 2),
                 "hbm_frac_whole_node": round(value / (HBM_PEAK_GBS * world), 4),
                 "verified_windows": verified,
+                "seed": seed,
+                "stepper": st["stepper"],
+                "lane_chunk": st["lane_chunk"],
+                "build": dgrep.build_info().split()[0][len("head="):],
+                "build_info": dgrep.build_info(),
             },
             "roofline": {
                 "bound": "hbm",
@@ -211,6 +231,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel_ms_avg": round(kern_ms, 4),
+                "kernel_ms_median": round(kern_med, 4),
+                "kernel_ms_min": round(float(np.min(kms)), 4),
+                "overflow_ms_avg": round(float(np.mean([x["overflow_ms"] for x in stats])), 4),
+                "overflow_lanes": int(st["overflow_lanes"]),
+                "timing": "HIP events on the launch stream around the scan kernel and the overflow pass "
+                          "(dgrep_last_kernel_ms), averaged over the timed steps",
                 "algorithmic_bytes_per_launch": int(n + STAGED_LINE_BYTES * count),
             },
             "cpu_baseline": cpu,

@@ -284,6 +284,12 @@ static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block mu
 static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>::C % Tune<StepTable>::B == 0,
               "chunk must be a multiple of the block");
+// the LDS slots pack a matching line's chunk-relative start and '\n' index in
+// 16 bits each (Emitter): no compiled or runtime chunk may exceed 32 KiB
+constexpr int kMaxLaneChunk = 32768;
+static_assert(Tune<StepSheng8>::C <= kMaxLaneChunk && Tune<StepTable>::C <= kMaxLaneChunk &&
+                  Tune<StepWide>::C <= kMaxLaneChunk,
+              "lane chunk above 32 KiB overflows the 16-bit LDS slot offsets");
 
 // chunks per lane: the table stepper runs two in lockstep while its table is
 // small (<= 64 states); a bigger table would lose more occupancy (the LDS
@@ -747,9 +753,11 @@ constexpr bool use_staging() {
 // (adaptive_chunk_bytes): the fixed chunks of the other steppers leave the
 // last round of tiles over the resident waves part-empty, which at 16-KiB
 // chunks costs up to a sixth of a 16-GiB split's time.
+// Only one-chunk-per-lane, unstaged steppers take the runtime chunk: the
+// two-chunk path (run_lane2) and the staged path are compiled for Tune::C.
 template <class Step, int TBL>
 constexpr bool adaptive_chunk() {
-  return Step::kKind == kStepSheng8 && !use_staging<Step, TBL>();
+  return Step::kKind == kStepSheng8 && !use_staging<Step, TBL>() && streams_of<Step, TBL>() == 1;
 }
 template <class Step, int TBL>
 __device__ __forceinline__ uint32_t lane_chunk(const ScanArgs& a) {
@@ -884,22 +892,50 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   }
 }
 
-// Lanes that owned more matching lines than their LDS slots: one thread per
-// such lane runs it again in direct-write mode (rare: dense short matches).
+// Lanes that owned more matching lines than their LDS slots are re-run here,
+// one WAVE per such lane chunk: the chunk is cut into up to 64 sub-chunks of
+// SC bytes (a multiple of the block) and sub-lane j applies the same
+// line-ownership rule to sub-chunk j (it owns the lines that start in it after
+// its first '\n'; sub-chunk 0 is the lane's own chunk start, so the lane's
+// lines are exactly the union). Pass 1 counts each sub-lane's matching lines
+// and '\n' (no writes), a wave scan turns the counts into offsets, pass 2
+// re-runs every sub-chunk writing its lines straight to their final staging
+// positions. Each chunk is read twice, but by 64 lanes at once, so dense
+// matches no longer serialise on one thread per chunk.
+constexpr int kOverflowThreads = 256;
 template <class Step, int TBL>
-__global__ __launch_bounds__(64) void scan_overflow_kernel(ScanArgs a, uint64_t nover) {
+__global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArgs a, uint64_t nover) {
   constexpr int E = Tune<Step>::E, BK = Tune<Step>::B;
   const uint32_t C = lane_chunk<Step, TBL>(a);
-  __shared__ ScanSmem<TBL, 1, 64> sm;
-  for (uint32_t i = threadIdx.x * 16u; i < a.table_bytes; i += 64 * 16u)
+  __shared__ ScanSmem<TBL, 1, 1> sm;
+  for (uint32_t i = threadIdx.x * 16u; i < a.table_bytes; i += kOverflowThreads * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
   __syncthreads();
   const Step st = make_step<Step>(sm.tbl, a);
-  for (uint64_t k = uint64_t(blockIdx.x) * 64 + threadIdx.x; k < nover; k += uint64_t(gridDim.x) * 64) {
-    const OverflowLane ol = a.overflow[k];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t sc = C / 64u;
+  sc = sc < uint32_t(BK) ? uint32_t(BK) : sc - sc % uint32_t(BK);
+  const uint32_t nsub = (C + sc - 1) / sc;  // <= 64 (C and sc are multiples of BK)
+  const uint64_t waves = uint64_t(gridDim.x) * (kOverflowThreads / 64);
+  for (uint64_t k = uint64_t(blockIdx.x) * (kOverflowThreads / 64) + (threadIdx.x >> 6); k < nover; k += waves) {
+    const OverflowLane ol = a.overflow[k];  // wave-uniform
+    const bool live = lane < nsub;
+    const uint64_t cs = ol.cs + uint64_t(lane) * sc;
+    const uint32_t len = live ? min(sc, C - lane * sc) : 0u;
     LaneRun r;
-    Emitter<E, true> ed{&a, nullptr, ol.cs, ol.out_base, ol.nl_prefix};
-    run_lane<BK>(a, st, ol.cs, r, ed, C);
+    uint32_t nl = 0, nev = 0;
+    if (live) {
+      // out_base = capacity: every write of the counting pass is skipped
+      Emitter<E, true> cnt{&a, nullptr, cs, a.capacity, 0};
+      nl = run_lane<BK>(a, st, cs, r, cnt, len);
+      nev = r.nev;
+    }
+    const uint32_t nl_off = wave_incl_scan(nl) - nl;
+    const uint32_t ev_off = wave_incl_scan(nev) - nev;
+    if (live && nev) {
+      Emitter<E, true> ed{&a, nullptr, cs, ol.out_base + ev_off, ol.nl_prefix + nl_off};
+      run_lane<BK>(a, st, cs, r, ed, len);
+    }
   }
 }
 
@@ -1020,9 +1056,10 @@ hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
 }
 template <class Step, int TBL>
 hipError_t overflow_t(const ScanArgs& a, uint64_t nover, hipStream_t stream) {
-  int grid = int((nover + 63) / 64);
-  if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL((scan_overflow_kernel<Step, TBL>), dim3(grid), dim3(64), 0, stream, a, nover);
+  constexpr uint64_t wpb = kOverflowThreads / 64;
+  int grid = int((nover + wpb - 1) / wpb);
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL((scan_overflow_kernel<Step, TBL>), dim3(grid), dim3(kOverflowThreads), 0, stream, a, nover);
   return hipGetLastError();
 }
 template <class Step, int TBL>
@@ -1049,10 +1086,15 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
 // chunk sized to fill whole rounds exactly) 4.13: keep powers of two. The LDS
 // slots pack a line's chunk-relative start (<= C) and '\n' index (<= C) in 16
 // bits each, so 32,768 is also the hard limit (65,536 fails GPU parity).
-constexpr uint64_t kShengMaxChunk = 32768;
-uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c) {
+// `dens_cap` (0 = none) is the largest chunk whose expected matching lines,
+// at the match density of the previous scan of this pattern, fill at most half
+// of a lane's LDS slots: a denser pattern keeps smaller chunks instead of
+// sending most lanes through the overflow pass.
+constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
+uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c, uint64_t dens_cap) {
   uint64_t c = floor_c;
-  while (c * 2 <= kShengMaxChunk && n >= waves * uint64_t(kTileLanes) * c * 2) c *= 2;
+  while (c * 2 <= kShengMaxChunk && n >= waves * uint64_t(kTileLanes) * c * 2 && (!dens_cap || c * 2 <= dens_cap))
+    c *= 2;
   return uint32_t(c);
 }
 struct TileOp {
@@ -1061,11 +1103,16 @@ struct TileOp {
   uint32_t* waves_per_block;
   uint64_t n, resident_blocks;
   uint32_t force;
+  double density;  // matching lines per byte seen by the previous scan (0: unknown)
+  uint32_t* slots;
   template <class S, int T>
   hipError_t run() const {
     uint64_t c = uint64_t(Tune<S>::C);
+    *slots = uint32_t(Tune<S>::E);
+    const uint64_t dens_cap = density > 0 ? uint64_t(double(Tune<S>::E) / (2.0 * density)) : 0;
     if constexpr (adaptive_chunk<S, T>())
-      c = force ? uint64_t(force) : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c);
+      c = force ? uint64_t(force)
+                : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap);
     *chunk = uint32_t(c);
     *waves_per_block = uint32_t(threads_of<S>() / 64);
     *bytes = uint64_t(kTileLanes) * uint64_t(streams_of<S, T>()) * c;
@@ -1094,9 +1141,9 @@ struct OverflowOp {
 }  // namespace
 
 uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t resident_blocks, uint32_t force,
-                         uint32_t* chunk, uint32_t* waves_per_block) {
+                         double density, uint32_t* chunk, uint32_t* waves_per_block, uint32_t* slots) {
   uint64_t b = 0;
-  (void)dispatch(kind, table_bytes, TileOp{&b, chunk, waves_per_block, n, resident_blocks, force});
+  (void)dispatch(kind, table_bytes, TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots});
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {

@@ -31,7 +31,7 @@
 namespace dgrep {
 // scan_dfa.hip
 uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t resident_blocks, uint32_t force,
-                         uint32_t* chunk, uint32_t* waves_per_block);
+                         double density, uint32_t* chunk, uint32_t* waves_per_block, uint32_t* slots);
 uint32_t scan_table_row();
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu);
 hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
@@ -87,8 +87,12 @@ struct dgrep_ctx {
   uint32_t* d_res_len = nullptr;
   uint64_t res_cap = 0;
 
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   float last_ms = 0.f;
+  dgrep_scan_stats stats{};
+  // matching lines per byte of the last scan of the loaded pattern (0 after
+  // dgrep_load_dfa): caps the adaptive lane chunk (scan_tile_bytes)
+  double density = 0.0;
 
   // dgrep_scan ingest (worker split -> HBM): host bytes are copied by
   // `ingest_threads` CPU threads into one of `ingest_bufs` pinned staging
@@ -157,6 +161,8 @@ extern "C" int dgrep_open(int device, dgrep_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev2);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev3);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), 4 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     // keep the context so the caller can read the message
@@ -186,6 +192,8 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  if (c->ev3) (void)hipEventDestroy(c->ev3);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -311,6 +319,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   int bpc = 0;
   HIPCHK(scan_dfa_occupancy(c->step_kind, c->table_bytes, &bpc));
   c->blocks_per_cu = std::max(1, bpc);
+  c->density = 0.0;
   c->loaded = true;
   return DGREP_OK;
 }
@@ -340,8 +349,9 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     return DGREP_E_INVALID;
   }
   const uint64_t resident = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
-  uint32_t chunk = 0, wpb = 1;
-  const uint64_t tile = scan_tile_bytes(c->step_kind, c->table_bytes, n, resident, c->lane_chunk, &chunk, &wpb);
+  uint32_t chunk = 0, wpb = 1, slots = 0;
+  const uint64_t tile = scan_tile_bytes(c->step_kind, c->table_bytes, n, resident, c->lane_chunk, c->density, &chunk,
+                                        &wpb, &slots);
   const uint64_t ntiles = (n + tile - 1) / tile;
   int rc;
   if ((rc = grow(c, &c->d_tiles, &c->tiles_cap, ntiles)) != DGREP_OK) return rc;
@@ -378,6 +388,12 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   (void)wpb;
   const int grid = int(std::min<uint64_t>(ntiles, resident));
   unsigned long long ctr[4] = {0, 0, 0, 0};
+  dgrep_scan_stats& S = c->stats;
+  S = dgrep_scan_stats{};
+  S.stepper = uint32_t(c->step_kind);
+  S.lane_chunk = chunk;
+  S.lane_slots = slots;
+  S.tiles = ntiles;
   for (int attempt = 0; attempt < 2; ++attempt) {
     a.overflow = c->d_overflow;
     a.overflow_cap = c->overflow_cap;
@@ -387,22 +403,38 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     HIPCHK(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    S.scan_ms += ms;  // a re-run scan is counted: it is part of this call's device time
+    ++S.scan_attempts;
     if (ctr[1] <= c->overflow_cap) break;
     // more overflowing lanes than recorded: grow the list and scan again
     if ((rc = grow(c, &c->d_overflow, &c->overflow_cap, ctr[1])) != DGREP_OK) return rc;
   }
-  HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
   const uint64_t total = ctr[0];
+  S.overflow_lanes = ctr[1];
+  S.matches = total;
+  c->last_ms = S.scan_ms;
   if (uint32_t(ctr[2]) & kStatusLineTooLong) {
     c->err = "a matching line is longer than 4 GiB (uint32 length in dgrep_result)";
     return DGREP_E_UNSUPPORTED;
   }
-  if (ctr[1] && total <= capacity) HIPCHK(scan_dfa_overflow(c->step_kind, a, ctr[1], c->stream));
+  c->density = double(total) / double(n);
+  const bool over = ctr[1] && total <= capacity;
+  if (over) {
+    HIPCHK(hipEventRecord(c->ev2, c->stream));
+    HIPCHK(scan_dfa_overflow(c->step_kind, a, ctr[1], c->stream));
+    HIPCHK(hipEventRecord(c->ev3, c->stream));
+  }
   *count = total;
-  if (total == 0 || total > capacity) return DGREP_OK;
-  HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->d_blk, capacity, d_line,
-                     d_start, d_len, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (total != 0 && total <= capacity)
+    HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->d_blk, capacity, d_line,
+                       d_start, d_len, c->stream));
+  if (over || (total != 0 && total <= capacity)) HIPCHK(hipStreamSynchronize(c->stream));
+  if (over) {
+    HIPCHK(hipEventElapsedTime(&S.overflow_ms, c->ev2, c->ev3));
+    c->last_ms += S.overflow_ms;
+  }
   return DGREP_OK;
 }
 
@@ -727,6 +759,13 @@ extern "C" int dgrep_last_kernel_ms(dgrep_ctx* c, float* ms) {
   *ms = c->last_ms;
   return DGREP_OK;
 }
+
+extern "C" int dgrep_last_scan_stats(dgrep_ctx* c, dgrep_scan_stats* out) {
+  if (!c || !out) return DGREP_E_INVALID;
+  *out = c->stats;
+  return DGREP_OK;
+}
+
 
 // ---- synthetic corpus ------------------------------------------------------
 __global__ void synth_kernel(char* out, uint64_t n, uint64_t seed, int kind) {

@@ -53,8 +53,10 @@ EXPORTS = (
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
     "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_lane_chunk", "dgrep_set_ingest", "dgrep_last_ingest_ms",
     "dgrep_map_partitions", "dgrep_partitions_free", "dgrep_encode_device", "dgrep_last_encode_ms",
-    "dgrep_reduce", "dgrep_reduce_free",
+    "dgrep_reduce", "dgrep_reduce_free", "dgrep_last_scan_stats", "dgrep_build_info",
 )
+
+STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair"}
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
 
@@ -81,6 +83,12 @@ class _Partitions(ctypes.Structure):
 
 class _ReduceOut(ctypes.Structure):
     _fields_ = [("lines_in", ctypes.c_uint64), ("total", ctypes.c_uint64), ("bytes", ctypes.c_void_p)]
+
+
+class _ScanStats(ctypes.Structure):
+    _fields_ = [("stepper", ctypes.c_uint32), ("lane_chunk", ctypes.c_uint32), ("lane_slots", ctypes.c_uint32),
+                ("scan_attempts", ctypes.c_uint32), ("tiles", ctypes.c_uint64), ("overflow_lanes", ctypes.c_uint64),
+                ("matches", ctypes.c_uint64), ("scan_ms", ctypes.c_float), ("overflow_ms", ctypes.c_float)]
 
 
 class _BlobInfo(ctypes.Structure):
@@ -153,6 +161,10 @@ def lib() -> ctypes.CDLL:
             L.dgrep_reduce.restype = i
             L.dgrep_reduce_free.argtypes = [ctypes.POINTER(_ReduceOut)]
             L.dgrep_reduce_free.restype = None
+            L.dgrep_last_scan_stats.argtypes = [vp, ctypes.POINTER(_ScanStats)]
+            L.dgrep_last_scan_stats.restype = i
+            L.dgrep_build_info.argtypes = []
+            L.dgrep_build_info.restype = ctypes.c_char_p
             _lib = L
     return _lib
 
@@ -342,6 +354,19 @@ class Context:
         ms = ctypes.c_float()
         self._check(self._L.dgrep_last_kernel_ms(self._h, ctypes.byref(ms)))
         return float(ms.value)
+
+    def scan_stats(self) -> dict:
+        """dgrep_last_scan_stats of the last scan (stepper, lane chunk, overflow lanes, times)."""
+        st = _ScanStats()
+        self._check(self._L.dgrep_last_scan_stats(self._h, ctypes.byref(st)))
+        d = {f: getattr(st, f) for f, _ in _ScanStats._fields_}
+        d["stepper"] = STEPPERS.get(d["stepper"], d["stepper"])
+        return d
+
+
+def build_info() -> str:
+    """dgrep_build_info(): "head=<commit>[-dirty] arch=gfx950 hipflags=..."."""
+    return lib().dgrep_build_info().decode()
 
 
 def synth_corpus_host(n: int, seed: int, kind: int = 0) -> bytes:

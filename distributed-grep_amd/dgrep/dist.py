@@ -4,46 +4,89 @@ gathered to the reducing rank.
 In the reference, each map task (one input file, map_reduce/coordinator.go:312,
 329-333) is scanned independently and its output travels to the reducers by
 SFTP (map_reduce/coordinator.go:136-142). Here one process per GPU scans its
-split in HBM and the compacted records — (line_no, start, len) per matching
-line, never the line bytes — are gathered to rank `dst` with torch.distributed
-(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for CPU tests). RCCL has no
-gatherv: counts are all-gathered first, records are padded to the largest
-count and gathered in one collective.
+split in HBM and the compacted records -- never the line bytes -- go to rank
+`dst` with torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo"
+in the CPU tests).
+
+The exchange: RCCL has no gatherv, so
+  1. the per-rank record counts are all-gathered (one 8-byte element per rank);
+  2. every rank packs its records into 20-byte records {u64 line_no, u64 start,
+     u32 len} (5 int32 words, on the device), and the senders' records move
+     with grouped point-to-point send/recv (batch_isend_irecv) straight into
+     one buffer on `dst`, in rank order -- exactly sum(counts) x 20 bytes cross
+     xGMI, each sender on its own link; nothing is padded to the largest count.
+Only `dst` turns the gathered counts into host integers (it must size its
+receive buffers); the senders already hold their own count, which
+dgrep_scan_device returns.
 """
 from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
+REC_WORDS = 5  # int32 words per record: line_no (2), start (2), len (1) = 20 B
+REC_BYTES = 4 * REC_WORDS
 
-def pack_records(line_no: torch.Tensor, start: torch.Tensor, length: torch.Tensor, count: int,
-                 width: int) -> torch.Tensor:
-    """[3, width] int64: rows line_no / start / len, zero-padded past `count`."""
-    rec = torch.zeros((3, max(width, 1)), dtype=torch.int64, device=line_no.device)
-    if count:
-        rec[0, :count] = line_no[:count].to(torch.int64)
-        rec[1, :count] = start[:count].to(torch.int64)
-        rec[2, :count] = length[:count].to(torch.int64)
-    return rec
+
+def pack_records(line_no: torch.Tensor, start: torch.Tensor, length: torch.Tensor, count: int) -> torch.Tensor:
+    """[count * 5] int32 on the records' device: per record the little-endian
+    words of (u64 line_no, u64 start, u32 len)."""
+    dev = line_no.device
+    if count == 0:
+        return torch.empty(0, dtype=torch.int32, device=dev)
+    ln = line_no[:count].to(torch.int64).contiguous().view(torch.int32).view(count, 2)
+    st = start[:count].to(torch.int64).contiguous().view(torch.int32).view(count, 2)
+    le = length[:count].to(torch.int32).contiguous().view(count, 1)
+    return torch.cat([ln, st, le], dim=1).reshape(-1)
+
+
+def unpack_records(buf: torch.Tensor, count: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Inverse of pack_records: (line_no int64, start int64, len int32)."""
+    r = buf[: count * REC_WORDS].view(count, REC_WORDS)
+    def words(lo, hi):
+        # a fresh dense copy: 8-byte aligned and contiguous whatever the slice was
+        t = torch.empty((count, hi - lo), dtype=torch.int32, device=buf.device)
+        t.copy_(r[:, lo:hi])
+        return t
+
+    ln = words(0, 2).view(torch.int64).reshape(-1)
+    st = words(2, 4).view(torch.int64).reshape(-1)
+    le = words(4, 5).reshape(-1)
+    return ln, st, le
 
 
 def gather_records(line_no: torch.Tensor, start: torch.Tensor, length: torch.Tensor, count: int,
                    dst: int = 0, group=None) -> Optional[List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]]:
     """Gather every rank's match records to `dst`. Returns, on `dst`, one
-    (line_no, start, len) triple per rank in rank order (each trimmed to that
-    rank's count); None elsewhere."""
+    (line_no, start, len) triple per rank in rank order (each exactly that
+    rank's count long); None elsewhere. `dst` and the peers are global ranks."""
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    rank = dist.get_rank()
+    ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
     dev = line_no.device
     cnt = torch.tensor([count], dtype=torch.int64, device=dev)
-    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    counts = [torch.empty(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
-    width = max(counts)
-    rec = pack_records(line_no, start, length, count, width)
-    if rank == dst:
-        bufs = [torch.empty_like(rec) for _ in range(world)]
-        dist.gather(rec, gather_list=bufs, dst=dst, group=group)
-        return [(b[0, :c], b[1, :c], b[2, :c]) for b, c in zip(bufs, counts)]
-    dist.gather(rec, dst=dst, group=group)
-    return None
+    packed = pack_records(line_no, start, length, count)
+    if rank != dst:
+        if count:
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed, dst, group)]):
+                req.wait()
+        return None
+    cl = torch.cat(counts).tolist()  # the root sizes its receive buffer: its one host sync
+    total = sum(cl)
+    out = torch.empty(total * REC_WORDS, dtype=torch.int32, device=dev)
+    ops, off, views = [], 0, []
+    for peer, c in zip(ranks, cl):
+        seg = out[off * REC_WORDS:(off + c) * REC_WORDS]
+        views.append((seg, c))
+        if peer == dst:
+            if c:
+                seg.copy_(packed)
+        elif c:
+            ops.append(dist.P2POp(dist.irecv, seg, peer, group))
+        off += c
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return [unpack_records(seg, c) for seg, c in views]

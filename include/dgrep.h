@@ -185,9 +185,28 @@ int dgrep_synth_corpus(dgrep_ctx* ctx, void* d_out, size_t n, uint64_t seed, int
 int dgrep_synth_corpus_host(void* out, size_t n, uint64_t seed, int kind);
 /* Keyword i (0..999) of the seeded config-4 keyword set; returns its length. */
 int dgrep_synth_keyword(uint64_t seed, int i, char* out16);
-/* Average device time (ms) of the scan kernel over the last dgrep_scan*
- * call, measured with HIP events on the launch stream. */
+/* Device time (ms) of the last dgrep_scan* call's scan: the scan kernel
+ * (every attempt, if the overflow list had to grow) plus the overflow pass,
+ * measured with HIP events on the launch stream. */
 int dgrep_last_kernel_ms(dgrep_ctx* ctx, float* ms);
+
+/* What the last dgrep_scan* call did (tests, tuning, bench reports). */
+typedef struct {
+  uint32_t stepper;        /* 0 u8 table, 1 Sheng (<= 8 states), 2 wide u16 table, 3 pair (two bytes per lookup) */
+  uint32_t lane_chunk;     /* bytes per lane chunk */
+  uint32_t lane_slots;     /* LDS slots per lane chunk for matching lines */
+  uint32_t scan_attempts;  /* scan launches (2 if the overflow list had to grow) */
+  uint64_t tiles;          /* wave tiles of the split */
+  uint64_t overflow_lanes; /* lane chunks re-run by the overflow pass */
+  uint64_t matches;        /* matching lines */
+  float scan_ms;           /* scan kernel, all attempts */
+  float overflow_ms;       /* overflow pass */
+} dgrep_scan_stats;
+int dgrep_last_scan_stats(dgrep_ctx* ctx, dgrep_scan_stats* out);
+
+/* Provenance of this library: "head=<git commit>[-dirty] arch=gfx950
+ * hipflags=<tuning -D knobs>" (static string). */
+const char* dgrep_build_info(void);
 
 #ifdef __cplusplus
 }

@@ -74,3 +74,12 @@ def test_synth_host_deterministic_and_shaped():
     assert dgrep.synth_corpus_host(1 << 16, 6, 0) != a
     kws = dgrep.synth_keywords(4, 1000)
     assert len(set(kws)) > 990 and all(5 <= len(k) <= 12 and k.isalpha() and k.islower() for k in kws)
+
+
+def test_build_info_names_commit_and_arch():
+    """dgrep_build_info() stamps the commit the library was built from (the
+    bench reports it as config.build) and the tuning knobs compiled in."""
+    info = dgrep.build_info()
+    head = info.split()[0]
+    assert re.fullmatch(r"head=([0-9a-f]{40}(-dirty)?|unknown)", head), info
+    assert "arch=gfx950" in info and "hipflags=" in info

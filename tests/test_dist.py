@@ -1,7 +1,10 @@
 """Multi-rank path on CPU (gloo, world_size 2 and 4): the records each rank
-produces for its split are gathered to rank 0 unchanged and in rank order.
-The per-rank records come from the oracle here (the GPU scan is exercised in
-tests/test_gpu_parity.py); what is tested is the exchange step of bench.py."""
+produces for its split are gathered to the reducing rank unchanged and in rank
+order, with uneven counts (one rank 10x the others, one rank empty) and a
+non-zero destination rank. The per-rank records come from the oracle here
+(the GPU scan is exercised in tests/test_gpu_parity.py); what is tested is
+the exchange step of bench.py (dgrep/dist.py: count all-gather, then grouped
+send/recv of packed 20-byte records)."""
 import os
 import socket
 
@@ -9,6 +12,8 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -19,52 +24,89 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, os.path.join(root, "distributed-grep_amd"))
-    sys.path.insert(0, os.path.join(root, "tests"))
+def _split(rank):
+    """Rank r's split: rank 0 ten times the others, rank 1 none matching."""
     import dgrep
+
+    size = (2560 << 10) if rank == 0 else (256 << 10)
+    return dgrep.synth_corpus_host(size, 100 + rank, 0)
+
+
+def _records(rank):
     import oracle_lib as O
+
+    ln, st, le = O.grep_map(b"error", _split(rank))
+    if rank == 1:  # an empty contribution must be handled too
+        ln, st, le = ln[:0], st[:0], le[:0]
+    return ln, st, le
+
+
+def _worker(rank, world, port, dst, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     from dgrep.dist import gather_records
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        data = dgrep.synth_corpus_host(256 << 10, 100 + rank, 0)
-        ln, st, le = O.grep_map(b"error", data)
-        if rank == 1:  # an empty contribution must be handled too
-            ln, st, le = ln[:0], st[:0], le[:0]
-        t = [torch.from_numpy(x.astype("int64")) for x in (ln, st, le)]
-        out = gather_records(t[0], t[1], t[2], len(ln), dst=0)
-        if rank == 0:
+        ln, st, le = _records(rank)
+        # the scan's output arrays are longer than the count (capacity)
+        t = [torch.cat([torch.from_numpy(x.astype(dt)), torch.full((7,), -1, dtype=getattr(torch, dt))])
+             for x, dt in ((ln, "int64"), (st, "int64"), (le, "int32"))]
+        out = gather_records(t[0], t[1], t[2], len(ln), dst=dst)
+        if rank == dst:
             q.put([[x.tolist() for x in triple] for triple in out])
+        else:
+            assert out is None
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_gather_records_gloo(world):
+@pytest.mark.parametrize("world,dst", [(2, 0), (4, 0), (4, 2)])
+def test_gather_records_gloo(world, dst):
     import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "distributed-grep_amd"))
-    import dgrep
-    import oracle_lib as O
+    sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, dst, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    try:
+        got = q.get(timeout=150)
+    except Exception:
+        for p in procs:
+            p.join(timeout=5)
+        raise AssertionError("no result from rank %d; exit codes %s" % (dst, [p.exitcode for p in procs]))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert len(got) == world
+    total = 0
     for r in range(world):
-        data = dgrep.synth_corpus_host(256 << 10, 100 + r, 0)
-        ln, st, le = O.grep_map(b"error", data)
-        if r == 1:
-            ln, st, le = ln[:0], st[:0], le[:0]
-        assert got[r] == [ln.tolist(), st.tolist(), le.tolist()]
+        ln, st, le = _records(r)
+        assert got[r] == [ln.tolist(), st.tolist(), le.tolist()], r
+        total += len(ln)
+    n0 = len(_records(0)[0])
+    if world > 2:
+        assert n0 > 5 * max(len(_records(r)[0]) for r in range(2, world))  # uneven: rank 0 dominates
+    assert total > 0
+
+
+def test_pack_roundtrip():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
+    from dgrep.dist import REC_BYTES, pack_records, unpack_records
+
+    ln = torch.tensor([1, 2, (1 << 40) + 3], dtype=torch.int64)
+    st = torch.tensor([0, 17, (1 << 35) + 9], dtype=torch.int64)
+    le = torch.tensor([5, 0, 2**31 - 1], dtype=torch.int32)
+    p = pack_records(ln, st, le, 3)
+    assert p.numel() * 4 == 3 * REC_BYTES
+    a, b, c = unpack_records(p, 3)
+    assert a.tolist() == ln.tolist() and b.tolist() == st.tolist() and c.tolist() == le.tolist()
+    assert pack_records(ln, st, le, 0).numel() == 0

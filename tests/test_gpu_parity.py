@@ -185,6 +185,76 @@ def test_dense_matches_overflow_slots(gpu_ctx):
     _check(gpu_ctx, b"^$", data2)
 
 
+def _dense_lines(seed, count, maxlen):
+    rnd = random.Random(seed)
+    return b"\n".join(b"error WARN ab " + b"x" * rnd.randrange(maxlen) for _ in range(count))
+
+
+@pytest.mark.parametrize("chunk", [4096, 8192, 32768])
+def test_overflow_pass_dense_every_chunk(gpu_ctx, chunk):
+    """More matching lines per lane chunk than LDS slots at every Sheng chunk
+    shipped: the wave-parallel overflow pass (one wave per lane chunk, 64
+    sub-chunks, count pass + write pass) must give the oracle's records,
+    including lines that cross sub-chunk and chunk edges."""
+    try:
+        gpu_ctx.set_lane_chunk(chunk)
+        for maxlen in (4, 40, 700):
+            data = _dense_lines(chunk + maxlen, 40000 if maxlen < 100 else 8000, maxlen)
+            for pattern in (b"error", b"", b"b x"):
+                cp = gpu_ctx.load(pattern)
+                assert cp.nstates <= 8
+                _check(gpu_ctx, cp, data)
+                st = gpu_ctx.scan_stats()
+                assert st["stepper"] == "sheng" and st["lane_chunk"] == chunk
+                if maxlen < 100:
+                    assert st["overflow_lanes"] > 0, st
+    finally:
+        gpu_ctx.set_lane_chunk(0)
+
+
+@pytest.mark.parametrize("pattern", [b"(WARN|ERROR) [a-z_]+", b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+|error"])
+def test_overflow_pass_dense_table(gpu_ctx, pattern):
+    for maxlen in (4, 40, 700):
+        data = _dense_lines(maxlen, 30000 if maxlen < 100 else 6000, maxlen)
+        cp = gpu_ctx.load(pattern)
+        assert 8 < cp.nstates <= 256
+        _check(gpu_ctx, cp, data)
+        if maxlen < 100:
+            assert gpu_ctx.scan_stats()["overflow_lanes"] > 0
+
+
+def test_adaptive_chunk_on_large_split_and_density_cap(gpu_ctx):
+    """The adaptive Sheng chunk on a 2 GiB HBM-resident split (large enough to
+    select more than the compiled 4 KiB: dgrep_last_scan_stats reports it),
+    then a dense pattern: after its first scan the match density caps the
+    chunk. Every record is checked structurally and evenly spaced windows
+    (split start and end included) against the oracle (bench.verify_windows)."""
+    import torch
+    import bench
+
+    n = 2 << 30
+    buf = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    gpu_ctx.synth(buf.data_ptr(), n, 21, 0)
+    cap = 40 << 20
+    ln = torch.empty(cap, dtype=torch.int64, device="cuda")
+    st = torch.empty(cap, dtype=torch.int64, device="cuda")
+    le = torch.empty(cap, dtype=torch.int32, device="cuda")
+    chunks = {}
+    for pattern in ("error", "r"):
+        gpu_ctx.load(pattern)
+        for rep in range(2):
+            cnt = gpu_ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), cap)
+            assert 0 < cnt <= cap
+            s = gpu_ctx.scan_stats()
+            chunks[(pattern, rep)] = s["lane_chunk"]
+            assert bench.verify_windows(buf, n, ln[:cnt], st[:cnt], le[:cnt], pattern, 3, 1 << 20) == 3
+    assert chunks[("error", 0)] >= 8192 and chunks[("error", 1)] == chunks[("error", 0)], chunks
+    # "r" matches nearly every ~120-B line: 24 slots cap the chunk at the 4 KiB floor
+    assert chunks[("r", 0)] >= 8192 and chunks[("r", 1)] == 4096, chunks
+    del buf, ln, st, le
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("seed,pattern", [(1, b"error"), (2, b"timeout while waiting for lock"),
                                           (3, b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+")])
 def test_synth_corpus_vs_oracle(gpu_ctx, seed, pattern):
