@@ -51,6 +51,11 @@ struct ScanArgs {
   const uint16_t* wide;
   uint32_t nclasses;
   uint32_t hot_entries;
+  // kStepPair only (byte offsets into the LDS image, see StepPair)
+  uint32_t pair_t1;   // single-byte table T1
+  uint32_t pair_u;    // byte -> pair-index table U
+  uint32_t pair_thr;  // lowest premultiplied shadow state: a pair ending at >= thr holds an event
+  uint32_t pair_div;  // bytes per T2 row (2 * nclasses^2): premultiplied state / pair_div = state id
 };
 
 enum : uint32_t { kStatusLineTooLong = 1u };
@@ -63,7 +68,14 @@ enum : int {
   kStepTable = 0,   // <= 256 states: u8 [state][byte] table, 260-byte rows
   kStepSheng8 = 1,  // <= 8 states: per-byte 8-state vectors (v_perm stepping)
   kStepWide = 2,    // <= 65535 states: u16 [state][class] table, hot rows in LDS, all rows in HBM
+  kStepPair = 3,    // 2 * states * classes^2 <= kPairMaxT2 bytes: two input bytes per table lookup
 };
+
+// StepPair's two-byte table T2 (u16 [state][class][class], premultiplied
+// states) must address itself with 16-bit values; its whole LDS image (T2 +
+// T1 + the 1 KiB byte table) at most kPairMaxImage bytes.
+constexpr uint32_t kPairMaxT2 = 32768;
+constexpr uint32_t kPairMaxImage = 40960;
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
 // runtime renumbers states hottest-first (start, start_m, then BFS order from

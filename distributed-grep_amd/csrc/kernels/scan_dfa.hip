@@ -120,6 +120,19 @@
 #ifndef DGREP_NT_SHENG
 #define DGREP_NT_SHENG 0
 #endif
+// Pair (C3, 20 states): one chunk per lane, runtime (adaptive) chunk from 4 KiB
+#ifndef DGREP_PAIR_CHUNK
+#define DGREP_PAIR_CHUNK 4096
+#endif
+#ifndef DGREP_PAIR_SLOTS
+#define DGREP_PAIR_SLOTS 16
+#endif
+#ifndef DGREP_PAIR_BLOCK
+#define DGREP_PAIR_BLOCK 128
+#endif
+#ifndef DGREP_PAIR_WAVES
+#define DGREP_PAIR_WAVES 3
+#endif
 #ifndef DGREP_SHENG_SCHED_BARRIER
 #define DGREP_SHENG_SCHED_BARRIER 0
 #endif
@@ -251,8 +264,64 @@ struct StepWide {
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
 };
 
+// DFA whose two-byte table fits in LDS (2 * S' * K^2 <= kPairMaxT2 bytes; C3's
+// 20-state, 12-class regex: 6 KiB): ONE table lookup per TWO input bytes.
+//   T2 (LDS address 0): u16 [S'][K][K], entry = next state after the pair,
+//      PREMULTIPLIED to its row's byte offset (id * 2K^2), so the dependent
+//      chain per pair is one v_add + one ds_read_u16;
+//   U  (1 KiB): per byte b, 2K*class(b) | (2*class(b)) << 16, so the pair's
+//      column offset 2*(c1*K + c2) = lo16(U[b0]) + hi16(U[b1]) -- both
+//      lookups depend only on the input and are issued a word ahead; u32
+//      entries put byte b in bank b % 32 (text spreads over the banks);
+//   T1: u16 [S'][K] premultiplied single-byte steps (split tail, last-line check).
+// A pair hides the state between its two bytes, so a '\n' FIRST in a pair that
+// ends a matching line (the byte enters start_m) leads to a SHADOW state: a copy
+// of the state the second byte reaches, with its rows. The host numbers the
+// states so that shadows, start_m and shadow(start_m) are the highest: a
+// pair-end state >= thr means an event -- at its first byte if it is a shadow
+// other than start_m, at its second byte if it is >= M (start_m or its shadow).
+struct StepPair {
+  static constexpr int kKind = kStepPair;
+  const uint8_t* lds;
+  const uint32_t* U;
+  const uint16_t* T1;
+  uint32_t thr, M, div, K;
+  struct Pre {
+    uint32_t u0, u1, u2, u3;
+  };
+  __device__ __forceinline__ Pre prep(uint32_t x) const {
+    return Pre{U[x & 0xffu], U[(x >> 8) & 0xffu], U[(x >> 16) & 0xffu], U[x >> 24]};
+  }
+  __device__ __forceinline__ uint32_t t2(uint32_t off) const {
+    return *reinterpret_cast<const uint16_t*>(lds + off);
+  }
+  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                        uint32_t& s3) const {
+    const uint32_t pa = (p.u0 & 0xffffu) + (p.u1 >> 16);
+    const uint32_t pb = (p.u2 & 0xffffu) + (p.u3 >> 16);
+    s1 = t2(s + pa);
+    s3 = t2(s1 + pb);
+    s0 = s1;
+    s2 = s3;
+  }
+  // single-byte step (rare paths): state id = premultiplied state / row bytes
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return T1[(s / div) * K + (U[b] >> 17)]; }
+  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
+  __device__ __forceinline__ bool any2(uint32_t s1, uint32_t s3) const { return max(s1, s3) >= thr; }
+  // event bytes of a word whose pairs end in s1 (bytes 0-1) and s3 (bytes 2-3)
+  __device__ __forceinline__ uint32_t evm(uint32_t s1, uint32_t s3) const {
+    return uint32_t(s1 >= thr && s1 != M) | (uint32_t(s1 >= M) << 1) | (uint32_t(s3 >= thr && s3 != M) << 2) |
+           (uint32_t(s3 >= M) << 3);
+  }
+};
+
 template <class Step>
 __device__ __forceinline__ Step make_step(const uint8_t* lds, const ScanArgs& a);
+template <>
+__device__ __forceinline__ StepPair make_step<StepPair>(const uint8_t* lds, const ScanArgs& a) {
+  return StepPair{lds, reinterpret_cast<const uint32_t*>(lds + a.pair_u),
+                  reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div, a.nclasses};
+}
 template <>
 __device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }
 template <>
@@ -280,6 +349,12 @@ template <>
 struct Tune<StepWide> {
   static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK, S = DGREP_WIDE_STREAMS;
 };
+template <>
+struct Tune<StepPair> {
+  static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = 1;
+};
+static_assert(Tune<StepPair>::B == 64 || Tune<StepPair>::B == 128, "block must be 64 or 128 bytes");
+static_assert(Tune<StepPair>::C % Tune<StepPair>::B == 0 && Tune<StepPair>::C <= 32768, "bad pair chunk");
 static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>::C % Tune<StepTable>::B == 0,
@@ -367,7 +442,8 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
   // StepTable: keep each word's work in place (hoisting the chain-independent
   // newline masks of a whole block costs ~100 VGPRs). StepSheng8 wants the
   // opposite: its state-independent LDS reads should run ahead of the chain.
-  if (Step::kKind != kStepSheng8 || DGREP_SHENG_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);
+  if ((Step::kKind != kStepSheng8 && Step::kKind != kStepPair) || DGREP_SHENG_SCHED_BARRIER)
+    __builtin_amdgcn_sched_barrier(0);
   const uint32_t m = nl_mask(x);
   uint32_t s0, s1, s2, s3;
   st.apply(pre, s, s0, s1, s2, s3);
@@ -400,6 +476,8 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
   bool any;
   if constexpr (Step::kKind == kStepSheng8)
     any = StepSheng8::any4(s0, s1, s2, s3, M);
+  else if constexpr (Step::kKind == kStepPair)
+    any = st.any2(s1, s3);
   else
     any = bool(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)));
   if (__builtin_expect(any, 0)) {
@@ -408,8 +486,12 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
     const bool seen_w = r.seen || b.lastm != 0;
     const bool term_w = r.term || (b.past && b.lastm != 0);
     const int64_t prev_w = b.lastm ? int64_t(b.pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm)) : r.prev_nl;
-    uint32_t evm = uint32_t(Step::is(s0, M)) | (uint32_t(Step::is(s1, M)) << 1) | (uint32_t(Step::is(s2, M)) << 2) |
-                   (uint32_t(Step::is(s3, M)) << 3);
+    uint32_t evm;
+    if constexpr (Step::kKind == kStepPair)
+      evm = st.evm(s1, s3);
+    else
+      evm = uint32_t(Step::is(s0, M)) | (uint32_t(Step::is(s1, M)) << 1) | (uint32_t(Step::is(s2, M)) << 2) |
+            (uint32_t(Step::is(s3, M)) << 3);
     while (evm) {
       const uint32_t k = uint32_t(__builtin_ctz(evm));
       evm &= evm - 1;
@@ -757,7 +839,8 @@ constexpr bool use_staging() {
 // two-chunk path (run_lane2) and the staged path are compiled for Tune::C.
 template <class Step, int TBL>
 constexpr bool adaptive_chunk() {
-  return Step::kKind == kStepSheng8 && !use_staging<Step, TBL>() && streams_of<Step, TBL>() == 1;
+  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair) && !use_staging<Step, TBL>() &&
+         streams_of<Step, TBL>() == 1;
 }
 template <class Step, int TBL>
 __device__ __forceinline__ uint32_t lane_chunk(const ScanArgs& a) {
@@ -778,7 +861,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // waves per SIMD the register allocation must leave room for
 template <class Step>
 constexpr int waves_per_simd() {
-  return Step::kKind == kStepSheng8 ? DGREP_SHENG_WAVES : Step::kKind == kStepTable ? DGREP_TABLE_WAVES : kWideThreads / 256;
+  return Step::kKind == kStepSheng8  ? DGREP_SHENG_WAVES
+         : Step::kKind == kStepTable ? DGREP_TABLE_WAVES
+         : Step::kKind == kStepPair  ? DGREP_PAIR_WAVES
+                                     : kWideThreads / 256;
 }
 
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
@@ -913,8 +999,8 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
   __syncthreads();
   const Step st = make_step<Step>(sm.tbl, a);
   const uint32_t lane = threadIdx.x & 63u;
-  uint32_t sc = C / 64u;
-  sc = sc < uint32_t(BK) ? uint32_t(BK) : sc - sc % uint32_t(BK);
+  // sub-chunk: C / 64 rounded UP to a whole block, so at most 64 of them
+  const uint32_t sc = ((C + 63u) / 64u + uint32_t(BK) - 1u) / uint32_t(BK) * uint32_t(BK);
   const uint32_t nsub = (C + sc - 1) / sc;  // <= 64 (C and sc are multiples of BK)
   const uint64_t waves = uint64_t(gridDim.x) * (kOverflowThreads / 64);
   for (uint64_t k = uint64_t(blockIdx.x) * (kOverflowThreads / 64) + (threadIdx.x >> 6); k < nover; k += waves) {
@@ -1072,6 +1158,11 @@ hipError_t occ_t(int* b) {
 template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
+  if (kind == kStepPair) {
+    if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
+    if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
+    return op.template run<StepPair, int(kPairMaxImage)>();
+  }
   if (kind == kStepWide) return op.template run<StepWide, int(kWideClassBytes + kWideHotBytes)>();
   if (table_bytes <= 16 * kRow) return op.template run<StepTable, 16 * kRow>();
   if (table_bytes <= 32 * kRow) return op.template run<StepTable, 32 * kRow>();

@@ -27,6 +27,11 @@
 #ifndef DGREP_SHENG_MAX_STATES
 #define DGREP_SHENG_MAX_STATES 8
 #endif
+// DFAs above the Sheng limit whose two-byte table fits in LDS use the pair
+// stepper (0: they use the u8 table / wide steppers as before)
+#ifndef DGREP_PAIR_ENABLE
+#define DGREP_PAIR_ENABLE 1
+#endif
 
 namespace dgrep {
 // scan_dfa.hip
@@ -44,6 +49,11 @@ hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_
 
 using namespace dgrep;
 
+// StepPair image offsets and thresholds (see StepPair in scan_dfa.hip)
+struct PairArgs {
+  uint32_t t1 = 0, u = 0, thr = 0, div = 0;
+};
+
 struct dgrep_ctx {
   int device = 0;
   int num_cus = 0;
@@ -59,11 +69,13 @@ struct dgrep_ctx {
   uint32_t table_bytes = 0;
   uint16_t* d_wide = nullptr;  // kStepWide: the whole u16 [state][class] table
   uint32_t nclasses = 0, hot_entries = 0;
-  // dgrep_set_stepper: force the wide stepper / cap its LDS rows (tests, tuning)
-  bool force_wide = false;
+  // dgrep_set_stepper: force a stepper (0 auto, 1 wide, 2 u8 table, 3 pair) /
+  // cap the wide stepper's LDS rows (tests, tuning)
+  int force_stepper = 0;
   uint32_t wide_hot_rows_cap = UINT32_MAX;
   uint32_t lane_chunk = 0;  // dgrep_set_lane_chunk (0 = adaptive)
   int step_kind = kStepTable;
+  PairArgs pair_args;
   int blocks_per_cu = 1;
 
   // per-scan scratch (grown on demand, reused)
@@ -149,6 +161,77 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
   return DGREP_OK;
 }
 
+// The pair stepper's LDS image (StepPair, scan_dfa.hip) from the blob's DFA:
+// T2 u16 [S'][K][K] (two bytes per lookup), T1 u16 [S'][K] (single bytes),
+// U u32 [256] (byte -> column offsets), states premultiplied to their T2 row's
+// byte offset (id * 2K^2). S' = S + shadows: a pair whose FIRST byte is a '\n'
+// entering start_m hides that event in the state between its bytes, so it
+// leads to shadow(y) -- a copy of y = T[start_m][c2] -- instead of y. Ids:
+// the states other than start_m, then the shadows of y != start_m, then
+// start_m, then shadow(start_m): a pair-end id >= first shadow holds an
+// event. Returns false if the DFA does not fit (T2 > kPairMaxT2 bytes).
+bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::vector<uint8_t>* img, uint32_t* start,
+                      uint32_t* start_m, PairArgs* pa) {
+  const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
+  const uint32_t cn = h.byte_class[uint8_t('\n')];
+  auto T = [&](uint32_t s, uint32_t c) { return trans[size_t(s) * K + c]; };
+  // shadow targets, in class order
+  std::vector<uint32_t> shadow_of(S, UINT32_MAX);  // original state -> shadow id
+  std::vector<uint32_t> targets;
+  bool any_flag = false;
+  for (uint32_t s = 0; s < S; ++s) any_flag = any_flag || T(s, cn) == M;
+  if (any_flag)
+    for (uint32_t c = 0; c < K; ++c) {
+      const uint32_t y = T(M, c);
+      if (std::find(targets.begin(), targets.end(), y) == targets.end()) targets.push_back(y);
+    }
+  const uint32_t Sp = S + uint32_t(targets.size());
+  const uint64_t row = 2ull * K * K;  // bytes per T2 row
+  if (row * Sp > kPairMaxT2) return false;
+  const uint64_t t1_off = (row * Sp + 15) & ~15ull, u_off = (t1_off + 2ull * Sp * K + 15) & ~15ull;
+  if (u_off + 1024 > kPairMaxImage) return false;
+  std::vector<uint32_t> id(S), orig(Sp);
+  uint32_t next = 0;
+  for (uint32_t s = 0; s < S; ++s)
+    if (s != M) { id[s] = next; orig[next++] = s; }
+  const bool m_shadow = std::find(targets.begin(), targets.end(), M) != targets.end();
+  for (uint32_t y : targets)
+    if (y != M) { shadow_of[y] = next; orig[next++] = y; }
+  id[M] = next;
+  orig[next++] = M;
+  if (m_shadow) { shadow_of[M] = next; orig[next++] = M; }
+  // ids S-1 .. S'-1: the shadows of y != start_m, start_m, shadow(start_m)
+  const uint32_t thr_id = S - 1;
+  auto premul = [&](uint32_t i) { return uint16_t(uint64_t(i) * row); };
+  img->assign(u_off + 1024, 0);
+  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data());
+  uint16_t* t1 = reinterpret_cast<uint16_t*>(img->data() + t1_off);
+  uint32_t* u = reinterpret_cast<uint32_t*>(img->data() + u_off);
+  for (uint32_t i = 0; i < Sp; ++i) {
+    const uint32_t x = orig[i];
+    for (uint32_t c1 = 0; c1 < K; ++c1) {
+      const uint32_t a = T(x, c1);
+      const bool flagged = c1 == cn && a == M;
+      t1[size_t(i) * K + c1] = premul(id[a]);
+      for (uint32_t c2 = 0; c2 < K; ++c2) {
+        const uint32_t y = T(a, c2);
+        t2[(size_t(i) * K + c1) * K + c2] = premul(flagged ? shadow_of[y] : id[y]);
+      }
+    }
+  }
+  for (int b = 0; b < 256; ++b) {
+    const uint32_t c = h.byte_class[b];
+    u[b] = (2u * K * c) | ((2u * c) << 16);
+  }
+  *start = premul(id[h.start]);
+  *start_m = premul(id[M]);
+  pa->t1 = uint32_t(t1_off);
+  pa->u = uint32_t(u_off);
+  pa->thr = premul(thr_id);
+  pa->div = uint32_t(row);
+  return true;
+}
+
 }  // namespace
 
 extern "C" int dgrep_open(int device, dgrep_ctx** out) {
@@ -216,9 +299,9 @@ extern "C" int dgrep_set_lane_chunk(dgrep_ctx* c, uint32_t chunk_bytes) {
   return DGREP_OK;
 }
 
-extern "C" int dgrep_set_stepper(dgrep_ctx* c, int force_wide, uint32_t wide_hot_rows) {
-  if (!c) return DGREP_E_INVALID;
-  c->force_wide = force_wide != 0;
+extern "C" int dgrep_set_stepper(dgrep_ctx* c, int force, uint32_t wide_hot_rows) {
+  if (!c || force < 0 || force > 3) return DGREP_E_INVALID;
+  c->force_stepper = force;
   c->wide_hot_rows_cap = wide_hot_rows ? wide_hot_rows : UINT32_MAX;
   return DGREP_OK;
 }
@@ -248,7 +331,23 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   std::vector<uint8_t> t;
   std::vector<uint16_t> wide;
   uint32_t start = h.start, start_m = h.start_m;
-  if (h.nstates > 256 || c->force_wide) {
+  const int force = c->force_stepper;
+  std::vector<uint8_t> pair_img;
+  uint32_t pair_start = 0, pair_m = 0;
+  const bool pair_ok = (force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3
+                           ? build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args)
+                           : false;
+  if (force == 3 && !pair_ok) {
+    c->err = "dgrep_load_dfa: the pair stepper's two-byte table does not fit this DFA";
+    return DGREP_E_UNSUPPORTED;
+  }
+  if (pair_ok) {
+    c->step_kind = kStepPair;
+    c->nclasses = h.nclasses;
+    t.swap(pair_img);
+    start = pair_start;
+    start_m = pair_m;
+  } else if (h.nstates > 256 || force == 1) {
     // StepWide: renumber hottest-first -- start, start_m, then breadth-first
     // from start -- so the shallow states sit in the LDS-resident rows
     c->step_kind = kStepWide;
@@ -274,7 +373,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     t.assign((kWideClassBytes + size_t(c->hot_entries) * 2 + 15) & ~size_t(15), 0);
     memcpy(t.data(), h.byte_class, 256);
     memcpy(t.data() + kWideClassBytes, wide.data(), size_t(c->hot_entries) * 2);
-  } else if (h.nstates <= DGREP_SHENG_MAX_STATES) {
+  } else if (h.nstates <= DGREP_SHENG_MAX_STATES && force != 2) {
     // StepSheng8: V[b] = 8 bytes, byte s = next state of s on input byte b
     c->step_kind = kStepSheng8;
     // renumber so start_m is the highest state (the kernel tests a word's four
@@ -381,6 +480,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.wide = c->d_wide;
   a.nclasses = c->nclasses;
   a.hot_entries = c->hot_entries;
+  a.pair_t1 = c->pair_args.t1;
+  a.pair_u = c->pair_args.u;
+  a.pair_thr = c->pair_args.thr;
+  a.pair_div = c->pair_args.div;
   // every resident workgroup is launched even when the last round of tiles is
   // part-empty: trimming the grid so that every wave runs the same number of
   // tiles leaves some CUs with 2 workgroups and others with 3, and the time
