@@ -53,7 +53,6 @@ struct ScanArgs {
   uint32_t hot_entries;
   // kStepPair only (byte offsets into the LDS image, see StepPair)
   uint32_t pair_t1;   // single-byte table T1
-  uint32_t pair_u;    // byte -> pair-index table U
   uint32_t pair_thr;  // lowest premultiplied shadow state: a pair ending at >= thr holds an event
   uint32_t pair_div;  // bytes per T2 row (2 * nclasses^2): premultiplied state / pair_div = state id
 };
@@ -76,6 +75,7 @@ enum : int {
 // T1 + the 1 KiB byte table) at most kPairMaxImage bytes.
 constexpr uint32_t kPairMaxT2 = 32768;
 constexpr uint32_t kPairMaxImage = 40960;
+constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the two byte tables)
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
 // runtime renumbers states hottest-first (start, start_m, then BFS order from

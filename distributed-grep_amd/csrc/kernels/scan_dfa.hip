@@ -266,13 +266,15 @@ struct StepWide {
 
 // DFA whose two-byte table fits in LDS (2 * S' * K^2 <= kPairMaxT2 bytes; C3's
 // 20-state, 12-class regex: 6 KiB): ONE table lookup per TWO input bytes.
-//   T2 (LDS address 0): u16 [S'][K][K], entry = next state after the pair,
-//      PREMULTIPLIED to its row's byte offset (id * 2K^2), so the dependent
-//      chain per pair is one v_add + one ds_read_u16;
-//   U  (1 KiB): per byte b, 2K*class(b) | (2*class(b)) << 16, so the pair's
-//      column offset 2*(c1*K + c2) = lo16(U[b0]) + hi16(U[b1]) -- both
-//      lookups depend only on the input and are issued a word ahead; u32
+// LDS image (kPairT2 = 2 KiB of byte tables first, at LDS address 0):
+//   UA, UB (u32 [256] each): UA[b] = 2K*class(b), UB[b] = 2*class(b), so the
+//      pair's column offset 2*(c1*K + c2) = UA[b0] + UB[b1]; the four lookups
+//      of a word share one address (4*b, UB by the instruction's immediate
+//      offset), depend only on the input and are issued a word ahead; u32
 //      entries put byte b in bank b % 32 (text spreads over the banks);
+//   T2 (at kPairT2): u16 [S'][K][K], entry = next state after the pair,
+//      PREMULTIPLIED to its row's LDS address (kPairT2 + id * 2K^2), so the
+//      dependent chain per pair is one v_add3 + one ds_read_u16;
 //   T1: u16 [S'][K] premultiplied single-byte steps (split tail, last-line check).
 // A pair hides the state between its two bytes, so a '\n' FIRST in a pair that
 // ends a matching line (the byte enters start_m) leads to a SHADOW state: a copy
@@ -283,29 +285,34 @@ struct StepWide {
 struct StepPair {
   static constexpr int kKind = kStepPair;
   const uint8_t* lds;
-  const uint32_t* U;
   const uint16_t* T1;
   uint32_t thr, M, div, K;
   struct Pre {
-    uint32_t u0, u1, u2, u3;
+    uint32_t a0, b1, a2, b3;
   };
+  __device__ __forceinline__ uint32_t ua(uint32_t b) const {
+    return *reinterpret_cast<const uint32_t*>(lds + 4u * b);
+  }
+  __device__ __forceinline__ uint32_t ub(uint32_t b) const {
+    return *reinterpret_cast<const uint32_t*>(lds + 1024u + 4u * b);
+  }
   __device__ __forceinline__ Pre prep(uint32_t x) const {
-    return Pre{U[x & 0xffu], U[(x >> 8) & 0xffu], U[(x >> 16) & 0xffu], U[x >> 24]};
+    return Pre{ua(x & 0xffu), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu), ub(x >> 24)};
   }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
     return *reinterpret_cast<const uint16_t*>(lds + off);
   }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
-    const uint32_t pa = (p.u0 & 0xffffu) + (p.u1 >> 16);
-    const uint32_t pb = (p.u2 & 0xffffu) + (p.u3 >> 16);
-    s1 = t2(s + pa);
-    s3 = t2(s1 + pb);
+    s1 = t2(s + p.a0 + p.b1);
+    s3 = t2(s1 + p.a2 + p.b3);
     s0 = s1;
     s2 = s3;
   }
-  // single-byte step (rare paths): state id = premultiplied state / row bytes
-  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return T1[(s / div) * K + (U[b] >> 17)]; }
+  // single-byte step (rare paths): state id = (premultiplied state - kPairT2) / row bytes
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
+    return T1[((s - kPairT2) / div) * K + (ub(b) >> 1)];
+  }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
   __device__ __forceinline__ bool any2(uint32_t s1, uint32_t s3) const { return max(s1, s3) >= thr; }
   // event bytes of a word whose pairs end in s1 (bytes 0-1) and s3 (bytes 2-3)
@@ -319,8 +326,8 @@ template <class Step>
 __device__ __forceinline__ Step make_step(const uint8_t* lds, const ScanArgs& a);
 template <>
 __device__ __forceinline__ StepPair make_step<StepPair>(const uint8_t* lds, const ScanArgs& a) {
-  return StepPair{lds, reinterpret_cast<const uint32_t*>(lds + a.pair_u),
-                  reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div, a.nclasses};
+  return StepPair{lds, reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div,
+                  a.nclasses};
 }
 template <>
 __device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }

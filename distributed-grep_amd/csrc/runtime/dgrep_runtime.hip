@@ -51,7 +51,7 @@ using namespace dgrep;
 
 // StepPair image offsets and thresholds (see StepPair in scan_dfa.hip)
 struct PairArgs {
-  uint32_t t1 = 0, u = 0, thr = 0, div = 0;
+  uint32_t t1 = 0, thr = 0, div = 0;
 };
 
 struct dgrep_ctx {
@@ -162,9 +162,9 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 }
 
 // The pair stepper's LDS image (StepPair, scan_dfa.hip) from the blob's DFA:
-// T2 u16 [S'][K][K] (two bytes per lookup), T1 u16 [S'][K] (single bytes),
-// U u32 [256] (byte -> column offsets), states premultiplied to their T2 row's
-// byte offset (id * 2K^2). S' = S + shadows: a pair whose FIRST byte is a '\n'
+// UA, UB u32 [256] (byte -> column offsets), T2 u16 [S'][K][K] at kPairT2 (two
+// bytes per lookup), T1 u16 [S'][K] (single bytes); states premultiplied to
+// their T2 row's LDS address (kPairT2 + id * 2K^2). S' = S + shadows: a pair whose FIRST byte is a '\n'
 // entering start_m hides that event in the state between its bytes, so it
 // leads to shadow(y) -- a copy of y = T[start_m][c2] -- instead of y. Ids:
 // the states other than start_m, then the shadows of y != start_m, then
@@ -188,8 +188,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   const uint32_t Sp = S + uint32_t(targets.size());
   const uint64_t row = 2ull * K * K;  // bytes per T2 row
   if (row * Sp > kPairMaxT2) return false;
-  const uint64_t t1_off = (row * Sp + 15) & ~15ull, u_off = (t1_off + 2ull * Sp * K + 15) & ~15ull;
-  if (u_off + 1024 > kPairMaxImage) return false;
+  const uint64_t t1_off = (kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
+  if (end > kPairMaxImage) return false;
   std::vector<uint32_t> id(S), orig(Sp);
   uint32_t next = 0;
   for (uint32_t s = 0; s < S; ++s)
@@ -202,11 +202,12 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   if (m_shadow) { shadow_of[M] = next; orig[next++] = M; }
   // ids S-1 .. S'-1: the shadows of y != start_m, start_m, shadow(start_m)
   const uint32_t thr_id = S - 1;
-  auto premul = [&](uint32_t i) { return uint16_t(uint64_t(i) * row); };
-  img->assign(u_off + 1024, 0);
-  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data());
+  auto premul = [&](uint32_t i) { return uint16_t(kPairT2 + uint64_t(i) * row); };
+  img->assign(end, 0);
+  uint32_t* ua = reinterpret_cast<uint32_t*>(img->data());
+  uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + 1024);
+  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data() + kPairT2);
   uint16_t* t1 = reinterpret_cast<uint16_t*>(img->data() + t1_off);
-  uint32_t* u = reinterpret_cast<uint32_t*>(img->data() + u_off);
   for (uint32_t i = 0; i < Sp; ++i) {
     const uint32_t x = orig[i];
     for (uint32_t c1 = 0; c1 < K; ++c1) {
@@ -221,12 +222,12 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   }
   for (int b = 0; b < 256; ++b) {
     const uint32_t c = h.byte_class[b];
-    u[b] = (2u * K * c) | ((2u * c) << 16);
+    ua[b] = 2u * K * c;
+    ub[b] = 2u * c;
   }
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
   pa->t1 = uint32_t(t1_off);
-  pa->u = uint32_t(u_off);
   pa->thr = premul(thr_id);
   pa->div = uint32_t(row);
   return true;
@@ -481,7 +482,6 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.nclasses = c->nclasses;
   a.hot_entries = c->hot_entries;
   a.pair_t1 = c->pair_args.t1;
-  a.pair_u = c->pair_args.u;
   a.pair_thr = c->pair_args.thr;
   a.pair_div = c->pair_args.div;
   // every resident workgroup is launched even when the last round of tiles is

@@ -254,10 +254,15 @@ class Context:
         (dgrep_set_lane_chunk; 0 = adaptive)."""
         self._check(self._L.dgrep_set_lane_chunk(self._h, chunk_bytes))
 
-    def set_stepper(self, force_wide: bool = False, wide_hot_rows: int = 0):
-        """Testing/tuning: force the wide stepper and/or cap its LDS rows for
-        the next load() (dgrep_set_stepper)."""
-        self._check(self._L.dgrep_set_stepper(self._h, int(force_wide), wide_hot_rows))
+    _FORCE = {"auto": 0, "wide": 1, "table": 2, "pair": 3}
+
+    def set_stepper(self, force=False, wide_hot_rows: int = 0):
+        """Testing/tuning: the stepper the next load() uses (dgrep_set_stepper):
+        "auto" (default: by DFA size), "wide", "table" (u8, <= 256 states) or
+        "pair" (fails at load if its two-byte table does not fit); True/False
+        mean "wide"/"auto". wide_hot_rows caps the wide stepper's LDS rows."""
+        mode = self._FORCE[force] if isinstance(force, str) else int(bool(force))
+        self._check(self._L.dgrep_set_stepper(self._h, mode, wide_hot_rows))
 
     def load(self, pattern) -> CompiledPattern:
         cp = pattern if isinstance(pattern, CompiledPattern) else CompiledPattern(pattern)

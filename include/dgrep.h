@@ -92,15 +92,19 @@ const char* dgrep_last_error(dgrep_ctx* ctx);
 int dgrep_set_stream(dgrep_ctx* ctx, void* hip_stream);
 int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
 /* Stepper selection for later dgrep_load_dfa calls (tests / tuning only; the
- * default picks by state count: <= 8 Sheng, <= 256 u8 table, else wide).
- * force_wide != 0 uses the wide (u16, LDS-hot + HBM) stepper for any DFA;
- * wide_hot_rows != 0 caps its LDS-resident rows. */
-int dgrep_set_stepper(dgrep_ctx* ctx, int force_wide, uint32_t wide_hot_rows);
-/* Tests / tuning: lane chunk of the Sheng (<= 8-state) stepper for later
- * scans. 0 (default) = adaptive: the compiled 4 KiB chunk, doubled (up to
- * 32 KiB) while every resident wave still gets a tile; otherwise a multiple
- * of 128 in [4096, 32768] (LDS slots hold 16-bit chunk offsets). No effect
- * on other steppers. */
+ * default picks by size: <= 8 states Sheng; else the pair stepper if its
+ * two-byte table fits in LDS; else <= 256 states the u8 table; else wide).
+ * force: 0 = that default, 1 = wide (u16, LDS-hot + HBM) for any DFA, 2 = the
+ * u8 table (<= 256 states), 3 = pair (dgrep_load_dfa fails with
+ * DGREP_E_UNSUPPORTED if it does not fit). wide_hot_rows != 0 caps the wide
+ * stepper's LDS-resident rows. */
+int dgrep_set_stepper(dgrep_ctx* ctx, int force, uint32_t wide_hot_rows);
+/* Tests / tuning: lane chunk of the Sheng (<= 8-state) and pair steppers for
+ * later scans. 0 (default) = adaptive: the compiled 4 KiB chunk, doubled (up
+ * to 32 KiB) while every resident wave still gets a tile and the matching
+ * lines the previous scan's density predicts fill at most half of a lane's
+ * LDS slots; otherwise a multiple of 128 in [4096, 32768] (LDS slots hold
+ * 16-bit chunk offsets). No effect on the u8 table and wide steppers. */
 int dgrep_set_lane_chunk(dgrep_ctx* ctx, uint32_t chunk_bytes);
 
 /* Host bytes -> H2D -> scan -> D2H results. This is the call Map makes.

@@ -154,9 +154,14 @@ def test_table_stream_configs_at_edges(gpu_ctx, pattern):
         for edge in (2047, 2048, 4095, 4096, 131071, 131072, 262143, 262144):
             if edge < len(data):
                 data[edge] = 0x0A
-        cp = gpu_ctx.load(pattern)
-        assert 8 < cp.nstates <= 256
-        _check(gpu_ctx, cp, bytes(data))
+        try:
+            gpu_ctx.set_stepper("table")
+            cp = gpu_ctx.load(pattern)
+            assert 8 < cp.nstates <= 256
+            _check(gpu_ctx, cp, bytes(data))
+            assert gpu_ctx.scan_stats()["stepper"] == "table"
+        finally:
+            gpu_ctx.set_stepper("auto")
 
 
 def test_long_lines_cross_many_chunks(gpu_ctx):
@@ -214,13 +219,19 @@ def test_overflow_pass_dense_every_chunk(gpu_ctx, chunk):
 
 @pytest.mark.parametrize("pattern", [b"(WARN|ERROR) [a-z_]+", b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+|error"])
 def test_overflow_pass_dense_table(gpu_ctx, pattern):
-    for maxlen in (4, 40, 700):
-        data = _dense_lines(maxlen, 30000 if maxlen < 100 else 6000, maxlen)
-        cp = gpu_ctx.load(pattern)
-        assert 8 < cp.nstates <= 256
-        _check(gpu_ctx, cp, data)
-        if maxlen < 100:
-            assert gpu_ctx.scan_stats()["overflow_lanes"] > 0
+    try:
+        gpu_ctx.set_stepper("table")
+        for maxlen in (4, 40, 700):
+            data = _dense_lines(maxlen, 30000 if maxlen < 100 else 6000, maxlen)
+            cp = gpu_ctx.load(pattern)
+            assert 8 < cp.nstates <= 256
+            _check(gpu_ctx, cp, data)
+            st = gpu_ctx.scan_stats()
+            assert st["stepper"] == "table"
+            if maxlen < 100:
+                assert st["overflow_lanes"] > 0
+    finally:
+        gpu_ctx.set_stepper("auto")
 
 
 def test_adaptive_chunk_on_large_split_and_density_cap(gpu_ctx):
@@ -387,3 +398,77 @@ def test_keyword_alternation_c4(gpu_ctx, nkw, size):
     data = dgrep.synth_corpus_host(size, 4, 1)
     n = _check(gpu_ctx, cp, data, threads=16)
     assert n > 0
+
+
+# ---- the pair stepper (two bytes per LDS lookup, shadow states) -------------
+PAIR_PATTERNS = [b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"(WARN|ERROR) [a-z_]+",
+                 b"timeout while waiting for lock", b"\\bkey\\b", b"^[ -~]{45}$", b"e(r|x)+o", b"a|^$",
+                 b"[^a-z ]{3}", b"^$|error", b"x*$|WARN"]
+
+
+@pytest.mark.parametrize("pattern", PAIR_PATTERNS)
+def test_pair_stepper_edges_and_random(gpu_ctx, pattern):
+    cp = gpu_ctx.load(pattern)
+    for data in [b"", b"\n", b"\n\n", b"\n\n\n", b"x", b"x\n", b"\nx", b"error\n\nerror", b"key\nk\n",
+                 b"\xff\xfe\n\xe2\x82\xac\n\xe2\x82\n", b"a" * 5000 + b"WARN ab" + b"b" * 5000 + b"\nerror"]:
+        _check(gpu_ctx, cp, data)
+        assert gpu_ctx.scan_stats()["stepper"] == "pair", pattern
+    rnd = random.Random(hash(pattern) & 0xffff)
+    alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\n\n", b"\r",
+             b"\xe2\x82\xac", b"\xff", b"WARN ab", b"ERROR x", b"error", b"2024-01-02", b"key "]
+    for _ in range(12):
+        n = rnd.choice([10, 1000, 70000, 300000])
+        _check(gpu_ctx, cp, b"".join(rnd.choice(alpha) for _ in range(n // 3)))
+
+
+@pytest.mark.parametrize("chunk", [4096, 8192, 32768])
+def test_pair_stepper_chunk_and_tile_edges(gpu_ctx, chunk):
+    import dgrep
+
+    tile = 64 * chunk
+    try:
+        gpu_ctx.set_lane_chunk(chunk)
+        for size in (chunk - 1, chunk, chunk + 1, tile - 1, tile, tile + 1, 2 * tile + 777):
+            data = bytearray(dgrep.synth_corpus_host(size, 17, 0))
+            # '\n' first and second in a pair at chunk / tile edges and beside them
+            for edge in (chunk - 2, chunk - 1, chunk, chunk + 1, 2 * chunk, tile - 1, tile, tile + chunk):
+                if edge < size:
+                    data[edge] = 0x0A
+            if size > 3 * chunk:
+                data[chunk + 5:3 * chunk] = b"x" * (2 * chunk - 5)  # a line over two chunk edges
+                data[2 * chunk:2 * chunk + 8] = b" WARN ab"
+            data = bytes(data)
+            for pattern in (b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"^$|ok$", b"(WARN|ERROR) [a-z_]+"):
+                cp = gpu_ctx.load(pattern)
+                _check(gpu_ctx, cp, data)
+                st = gpu_ctx.scan_stats()
+                assert st["stepper"] == "pair" and st["lane_chunk"] == chunk, st
+    finally:
+        gpu_ctx.set_lane_chunk(0)
+
+
+def test_pair_stepper_dense_overflow(gpu_ctx):
+    for maxlen in (2, 5, 40, 700):
+        data = _dense_lines(maxlen + 1, 40000 if maxlen < 100 else 6000, maxlen)
+        for pattern in (b"(WARN|ERROR) [a-z_]+", b"^$|error", b"b x*$"):
+            cp = gpu_ctx.load(pattern)
+            _check(gpu_ctx, cp, data)
+            assert gpu_ctx.scan_stats()["stepper"] == "pair"
+    data2 = b"\n" * 100001
+    for pattern in (b"^$|error", b"a|^$"):
+        _check(gpu_ctx, pattern, data2)
+
+
+@pytest.mark.parametrize("mode", ["table", "pair", "wide"])
+def test_forced_steppers_agree_on_c3(gpu_ctx, mode):
+    """C3's regex through each stepper that can hold it (dgrep_set_stepper)."""
+    import dgrep
+
+    data = dgrep.synth_corpus_host(6 << 20, 3, 0)
+    try:
+        gpu_ctx.set_stepper(mode)
+        cp = gpu_ctx.load(b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+")
+        _check(gpu_ctx, cp, data, threads=16)
+        assert gpu_ctx.scan_stats()["stepper"] == mode
+    finally:
+        gpu_ctx.set_stepper("auto")
