@@ -429,11 +429,16 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
 static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64_t* d_line, uint64_t* d_start,
                          uint32_t* d_len, uint64_t capacity, uint64_t* count) {
   *count = 0;
+  dgrep_scan_stats& S = c->stats;
+  S = dgrep_scan_stats{};
+  S.stepper = uint32_t(c->step_kind);
+  c->last_ms = 0.f;
   if (c->flags & DGREP_DFA_MATCH_NONE) return DGREP_OK;
   if (n == 0) {
     // strings.Split("", "\n") == [""]: one empty line, line 1
     if (!c->empty_line_matches) return DGREP_OK;
     *count = 1;
+    S.matches = 1;
     if (capacity >= 1) {
       const uint64_t one = 1, zero = 0;
       const uint32_t zl = 0;
@@ -491,9 +496,6 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   (void)wpb;
   const int grid = int(std::min<uint64_t>(ntiles, resident));
   unsigned long long ctr[4] = {0, 0, 0, 0};
-  dgrep_scan_stats& S = c->stats;
-  S = dgrep_scan_stats{};
-  S.stepper = uint32_t(c->step_kind);
   S.lane_chunk = chunk;
   S.lane_slots = slots;
   S.tiles = ntiles;
