@@ -406,8 +406,17 @@ PAIR_PATTERNS = [b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"(WARN|ERROR) [a-
                  b"[^a-z ]{3}", b"^$|error", b"x*$|WARN"]
 
 
-@pytest.mark.parametrize("pattern", PAIR_PATTERNS)
-def test_pair_stepper_edges_and_random(gpu_ctx, pattern):
+@pytest.fixture
+def pair_ctx(gpu_ctx):
+    # the pair stepper also for DFAs the default gives to Sheng (<= 8 states)
+    gpu_ctx.set_stepper("pair")
+    yield gpu_ctx
+    gpu_ctx.set_stepper("auto")
+
+
+@pytest.mark.parametrize("pattern", PAIR_PATTERNS + [b"error", b"", b"^$", b"(?i)k", b"\\x{FFFD}"])
+def test_pair_stepper_edges_and_random(pair_ctx, pattern):
+    gpu_ctx = pair_ctx
     cp = gpu_ctx.load(pattern)
     for data in [b"", b"\n", b"\n\n", b"\n\n\n", b"x", b"x\n", b"\nx", b"error\n\nerror", b"key\nk\n",
                  b"\xff\xfe\n\xe2\x82\xac\n\xe2\x82\n", b"a" * 5000 + b"WARN ab" + b"b" * 5000 + b"\nerror"]:
