@@ -55,9 +55,29 @@ struct ScanArgs {
   uint32_t pair_t1;   // single-byte table T1
   uint32_t pair_thr;  // lowest premultiplied shadow state: a pair ending at >= thr holds an event
   uint32_t pair_div;  // bytes per T2 row (2 * nclasses^2): premultiplied state / pair_div = state id
+  // kStepFilter only: the premultiplied CAND_END state (a '\n' ends a line that
+  // left the LDS-resident part of the DFA: a candidate, verified afterwards)
+  uint32_t cand_end;
 };
 
-enum : uint32_t { kStatusLineTooLong = 1u };
+// verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids
+struct VerifyArgs {
+  const uint8_t* data;
+  const uint16_t* full;  // u16 [nstates][nclasses], HBM
+  const uint8_t* cls;    // [256] byte classes, HBM
+  uint32_t nclasses, start, start_m;
+  TileInfo* tiles;
+  uint64_t ntiles;
+  StagedLine* staging;
+  uint64_t staging_cap;
+  unsigned long long* removed;
+};
+
+// A staged line whose len has this bit set is a filter CANDIDATE (kStepFilter):
+// verify_kernel re-runs it on the whole DFA and keeps it only if it matches.
+constexpr uint32_t kCandidateBit = 0x80000000u;
+
+enum : uint32_t { kStatusLineTooLong = 1u, kStatusCandidateTooLong = 2u };
 
 constexpr int kScanThreads = 256;  // 4 waves per workgroup
 constexpr int kTileLanes = 64;     // a tile is one wave's 64 chunks
@@ -68,7 +88,17 @@ enum : int {
   kStepSheng8 = 1,  // <= 8 states: per-byte 8-state vectors (v_perm stepping)
   kStepWide = 2,    // <= 65535 states: u16 [state][class] table, hot rows in LDS, all rows in HBM
   kStepPair = 3,    // 2 * states * classes^2 <= kPairMaxT2 bytes: two input bytes per table lookup
+  kStepFilter = 4,  // > 256 states: the DFA's shallow part in LDS, lines that leave it verified afterwards
 };
+
+// LDS image of kStepFilter: 256 class bytes, then u16 [state][class] rows of the
+// filter DFA (its states premultiplied by the class count), at most this many
+// bytes in all -- with 1024 threads x 4 slots x 8 B the workgroup stays within
+// the CU's 160 KiB.
+#ifndef DGREP_FILTER_KIB
+#define DGREP_FILTER_KIB 124
+#endif
+constexpr uint32_t kFilterImageBytes = DGREP_FILTER_KIB * 1024;
 
 // StepPair's two-byte table T2 (u16 [state][class][class], premultiplied
 // states) must address itself with 16-bit values; its whole LDS image (T2 +

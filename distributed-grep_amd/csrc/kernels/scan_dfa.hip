@@ -133,6 +133,16 @@
 #ifndef DGREP_PAIR_WAVES
 #define DGREP_PAIR_WAVES 3
 #endif
+// Filter (C4, > 256 states): 1024-thread workgroups sharing one LDS image
+#ifndef DGREP_FILTER_CHUNK
+#define DGREP_FILTER_CHUNK 4096
+#endif
+#ifndef DGREP_FILTER_SLOTS
+#define DGREP_FILTER_SLOTS 4
+#endif
+#ifndef DGREP_FILTER_BLOCK
+#define DGREP_FILTER_BLOCK 64
+#endif
 #ifndef DGREP_SHENG_SCHED_BARRIER
 #define DGREP_SHENG_SCHED_BARRIER 0
 #endif
@@ -322,8 +332,57 @@ struct StepPair {
   }
 };
 
+// DFA of more than 256 states (large alternations, SURVEY config 4) as a
+// FILTER that lives wholly in LDS: the runtime keeps the DFA's shallowest
+// states (breadth-first from start, as many as kFilterImageBytes holds) and
+// sends every transition that leaves them to CAND, which on '\n' enters
+// CAND_END (a start-like state, like start_m). A line that never leaves the
+// shallow part is decided exactly (start_m on its '\n' iff it matches); a line
+// that does is emitted as a CANDIDATE (kCandidateBit) and verify_kernel re-runs
+// it on the whole DFA. For C4's 1,000 keywords the shallow part is depth <= 3
+// of the Aho-Corasick-like DFA and 0.8 % of the lines are candidates.
+// LDS: 256 class bytes, then u16 [state][class] rows, entries premultiplied by
+// the class count (entry index of the next state's row): the dependent chain
+// per byte is one v_add_lshl + one ds_read_u16; the class lookups depend only on
+// the input and are issued a word ahead. Ids: shallow states, CAND, start_m,
+// CAND_END -- an event is a state >= start_m.
+struct StepFilter {
+  static constexpr int kKind = kStepFilter;
+  const uint8_t* lds;
+  uint32_t C;  // premultiplied CAND_END
+  struct Pre {
+    uint32_t c0, c1, c2, c3;
+  };
+  __device__ __forceinline__ Pre prep(uint32_t x) const {
+    return Pre{lds[x & 0xffu], lds[(x >> 8) & 0xffu], lds[(x >> 16) & 0xffu], lds[x >> 24]};
+  }
+  __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t c) const {
+    return *reinterpret_cast<const uint16_t*>(lds + kWideClassBytes + 2u * (s + c));
+  }
+  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                        uint32_t& s3) const {
+    s0 = one(s, p.c0);
+    s1 = one(s0, p.c1);
+    s2 = one(s1, p.c2);
+    s3 = one(s2, p.c3);
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return one(s, lds[b]); }
+  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s >= M; }
+};
+
+// the candidate flag of an event state (kStepFilter: CAND_END)
+template <class Step>
+__device__ __forceinline__ bool cand_of(const Step& st, uint32_t s) {
+  if constexpr (Step::kKind == kStepFilter) return s == st.C;
+  return false;
+}
+
 template <class Step>
 __device__ __forceinline__ Step make_step(const uint8_t* lds, const ScanArgs& a);
+template <>
+__device__ __forceinline__ StepFilter make_step<StepFilter>(const uint8_t* lds, const ScanArgs& a) {
+  return StepFilter{lds, a.cand_end};
+}
 template <>
 __device__ __forceinline__ StepPair make_step<StepPair>(const uint8_t* lds, const ScanArgs& a) {
   return StepPair{lds, reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div,
@@ -356,6 +415,11 @@ template <>
 struct Tune<StepWide> {
   static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK, S = DGREP_WIDE_STREAMS;
 };
+template <>
+struct Tune<StepFilter> {
+  static constexpr int C = DGREP_FILTER_CHUNK, E = DGREP_FILTER_SLOTS, B = DGREP_FILTER_BLOCK, S = 1;
+};
+static_assert(Tune<StepFilter>::C % Tune<StepFilter>::B == 0 && Tune<StepFilter>::C <= 32768, "bad filter chunk");
 template <>
 struct Tune<StepPair> {
   static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = 1;
@@ -405,23 +469,27 @@ struct Emitter {
   uint64_t out_base;     // first staging index of this lane (direct mode)
   uint32_t nl_prefix;    // '\n' between tile start and chunk start (direct mode)
 
-  __device__ __forceinline__ void operator()(LaneRun& r, uint64_t q, int64_t start, uint32_t rel) const {
+  // cand: a filter candidate (kCandidateBit in len, verified afterwards)
+  __device__ __forceinline__ void operator()(LaneRun& r, uint64_t q, int64_t start, uint32_t rel,
+                                             bool cand = false) const {
     const uint64_t len = q - uint64_t(start);
+    const uint32_t lw = uint32_t(len) | (cand ? kCandidateBit : 0u);
     if (DIRECT) {
       const uint64_t o = out_base + r.nev;
       if (o < a->capacity) {
         StagedLine L;
         L.start = cs + uint64_t(start);
-        L.len = uint32_t(len);
+        L.len = lw;
         L.rel = nl_prefix + rel;
         a->staging[o] = L;
       }
     } else if (r.nev < uint32_t(E)) {
       // start <= C and rel <= C fit 16 bits each
       slots[r.nev * 2 + 0] = uint32_t(start) | (rel << 16);
-      slots[r.nev * 2 + 1] = uint32_t(len);
+      slots[r.nev * 2 + 1] = lw;
     }
     if (len > 0xffffffffull) atomicOr(a->status, kStatusLineTooLong);
+    if (cand && len >= uint64_t(kCandidateBit)) atomicOr(a->status, kStatusCandidateTooLong);
     ++r.nev;
   }
 };
@@ -485,6 +553,8 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
     any = StepSheng8::any4(s0, s1, s2, s3, M);
   else if constexpr (Step::kKind == kStepPair)
     any = st.any2(s1, s3);
+  else if constexpr (Step::kKind == kStepFilter)
+    any = max(max(s0, s1), max(s2, s3)) >= M;
   else
     any = bool(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)));
   if (__builtin_expect(any, 0)) {
@@ -507,7 +577,8 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
       if (b.past) ok = ok && !term_w && below == 0;  // only the first '\n' past the chunk end
       if (!ok) continue;
       const int64_t start = below ? int64_t(q0 + hi_byte(below)) + 1 : prev_w + 1;
-      emit(r, q0 + k, start, b.nl0 + b.nlrun + uint32_t(__popc(below)));
+      const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+      emit(r, q0 + k, start, b.nl0 + b.nlrun + uint32_t(__popc(below)), cand_of(st, sk));
     }
   }
   if constexpr (TRACK) {
@@ -646,7 +717,7 @@ __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8
     const uint32_t b = p[pos];
     const uint32_t s1 = st.byte(r.s, b);
     if (b == '\n') {
-      if (Step::is(s1, M) && r.seen && !(pos >= C && r.term)) emit(r, pos, r.prev_nl + 1, r.nl);
+      if (Step::is(s1, M) && r.seen && !(pos >= C && r.term)) emit(r, pos, r.prev_nl + 1, r.nl, cand_of(st, s1));
       r.seen = true;
       ++r.nl;
       r.prev_nl = int64_t(pos);
@@ -654,7 +725,8 @@ __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8
     }
     r.s = s1;
   }
-  if (!r.term && r.seen && Step::is(st.byte(r.s, uint32_t('\n')), M)) emit(r, avail, r.prev_nl + 1, r.nl);
+  const uint32_t se = st.byte(r.s, uint32_t('\n'));
+  if (!r.term && r.seen && Step::is(se, M)) emit(r, avail, r.prev_nl + 1, r.nl, cand_of(st, se));
 }
 
 __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRun& r) {
@@ -680,7 +752,8 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   const uint64_t avail = cs < a.n ? a.n - cs : 0;
   if (avail <= pos0) {
     // the split ends exactly here: strings.Split's final piece
-    if (!r.term && r.seen && Step::is(st.byte(r.s, uint32_t('\n')), M)) emit(r, avail, r.prev_nl + 1, r.nl);
+    const uint32_t se = st.byte(r.s, uint32_t('\n'));
+    if (!r.term && r.seen && Step::is(se, M)) emit(r, avail, r.prev_nl + 1, r.nl, cand_of(st, se));
     return r.nl;
   }
   const uint8_t* __restrict__ p = a.data + cs;
@@ -846,8 +919,8 @@ constexpr bool use_staging() {
 // two-chunk path (run_lane2) and the staged path are compiled for Tune::C.
 template <class Step, int TBL>
 constexpr bool adaptive_chunk() {
-  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair) && !use_staging<Step, TBL>() &&
-         streams_of<Step, TBL>() == 1;
+  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepFilter) &&
+         !use_staging<Step, TBL>() && streams_of<Step, TBL>() == 1;
 }
 template <class Step, int TBL>
 __device__ __forceinline__ uint32_t lane_chunk(const ScanArgs& a) {
@@ -871,7 +944,7 @@ constexpr int waves_per_simd() {
   return Step::kKind == kStepSheng8  ? DGREP_SHENG_WAVES
          : Step::kKind == kStepTable ? DGREP_TABLE_WAVES
          : Step::kKind == kStepPair  ? DGREP_PAIR_WAVES
-                                     : kWideThreads / 256;
+                                     : kWideThreads / 256;  // wide, filter: one 1024-thread workgroup per CU
 }
 
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
@@ -1032,6 +1105,52 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
   }
 }
 
+// ---- filter verification (kStepFilter) -------------------------------------
+// One wave per tile: every candidate line (kCandidateBit) of the tile's staged
+// lines is re-run from its start on the WHOLE DFA (u16 [state][class] in HBM,
+// L2-resident; classes in LDS) and kept iff the '\n' after it enters start_m
+// (grep.go:21 on that line); the tile's kept lines are compacted in place, in
+// order, and its count updated; `removed` receives the dropped candidates.
+__global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
+  __shared__ uint8_t cls[256];
+  cls[threadIdx.x] = v.cls[threadIdx.x];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t waves = uint64_t(gridDim.x) * 4;
+  const uint32_t K = v.nclasses, cn = cls['\n'];
+  const __attribute__((address_space(1))) uint16_t* full = (const __attribute__((address_space(1))) uint16_t*)v.full;
+  for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
+    const TileInfo ti = v.tiles[t];
+    if (ti.count == 0) continue;
+    uint32_t kept = 0;
+    for (uint32_t k0 = 0; k0 < ti.count; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      const uint64_t src = ti.base + k;
+      bool keep = false;
+      StagedLine L;
+      if (k < ti.count && src < v.staging_cap) {
+        L = v.staging[src];
+        keep = true;
+        if (L.len & kCandidateBit) {
+          L.len &= ~kCandidateBit;
+          const uint8_t* p = v.data + L.start;
+          uint32_t st = v.start;
+          for (uint32_t i = 0; i < L.len; ++i) st = full[st * K + cls[p[i]]];
+          keep = full[st * K + cn] == v.start_m;
+        }
+      }
+      const uint64_t m = __ballot(keep);
+      const uint32_t pos = uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
+      if (keep) v.staging[ti.base + kept + pos] = L;  // in place: never beyond this batch's reads
+      kept += uint32_t(__popcll(m));
+    }
+    if (lane == 0 && kept != ti.count) {
+      v.tiles[t].count = kept;
+      atomicAdd(v.removed, (unsigned long long)(ti.count - kept));
+    }
+  }
+}
+
 // ---- ordering passes ------------------------------------------------------
 // Tiles append their lines to the staging buffer in atomic order; these passes
 // compute, per tile, its first output index (exclusive scan of counts) and the
@@ -1115,8 +1234,9 @@ __global__ __launch_bounds__(kOrdThreads) void tile_offsets_kernel(const TileInf
 // pass 4: one wave per tile copies its staged lines to their final slots (SoA)
 __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles, const StagedLine* staging,
                                                           uint64_t ntiles, const uint64_t* out_off,
-                                                          const uint64_t* line_base, uint64_t capacity,
-                                                          uint64_t* line_no, uint64_t* start, uint32_t* len) {
+                                                          const uint64_t* line_base, uint64_t staging_cap,
+                                                          uint64_t capacity, uint64_t* line_no, uint64_t* start,
+                                                          uint32_t* len) {
   const uint64_t waves = uint64_t(gridDim.x) * 4;
   for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles; t += waves) {
     const TileInfo ti = tiles[t];
@@ -1124,7 +1244,7 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
     const uint64_t o = out_off[t], lb = line_base[t];
     for (uint32_t k = threadIdx.x & 63; k < ti.count; k += 64) {
       const uint64_t src = ti.base + k, dst = o + k;
-      if (src < capacity && dst < capacity) {
+      if (src < staging_cap && dst < capacity) {
         const StagedLine L = staging[src];
         line_no[dst] = lb + L.rel;
         start[dst] = L.start;
@@ -1140,7 +1260,9 @@ uint32_t scan_table_row() { return kRow; }
 
 namespace {
 template <class Step>
-constexpr int threads_of() { return Step::kKind == kStepWide ? kWideThreads : kScanThreads; }
+constexpr int threads_of() {
+  return Step::kKind == kStepWide || Step::kKind == kStepFilter ? kWideThreads : kScanThreads;
+}
 template <class Step, int TBL>
 hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
   constexpr int NT = threads_of<Step>();
@@ -1171,6 +1293,7 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
     return op.template run<StepPair, int(kPairMaxImage)>();
   }
   if (kind == kStepWide) return op.template run<StepWide, int(kWideClassBytes + kWideHotBytes)>();
+  if (kind == kStepFilter) return op.template run<StepFilter, int(kFilterImageBytes)>();
   if (table_bytes <= 16 * kRow) return op.template run<StepTable, 16 * kRow>();
   if (table_bytes <= 32 * kRow) return op.template run<StepTable, 32 * kRow>();
   if (table_bytes <= 64 * kRow) return op.template run<StepTable, 64 * kRow>();
@@ -1258,8 +1381,8 @@ uint64_t order_blocks(uint64_t ntiles) { return (ntiles + kOrdTiles - 1) / kOrdT
 
 // out_off / line_base: ntiles entries; blk: 2 * order_blocks(ntiles) scratch
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
-                       uint64_t* line_base, uint64_t* blk, uint64_t capacity, uint64_t* line_no, uint64_t* start,
-                       uint32_t* len, hipStream_t stream) {
+                       uint64_t* line_base, uint64_t* blk, uint64_t staging_cap, uint64_t capacity,
+                       uint64_t* line_no, uint64_t* start, uint32_t* len, hipStream_t stream) {
   const uint64_t nblk = order_blocks(ntiles);
   uint64_t* blk_cnt = blk;
   uint64_t* blk_nl = blk + nblk;
@@ -1270,7 +1393,15 @@ hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_
   uint64_t grid = (ntiles + 3) / 4;
   if (grid > 16384) grid = 16384;
   hipLaunchKernelGGL(order_lines_kernel, dim3(grid), dim3(256), 0, stream, tiles, staging, ntiles, out_off,
-                     line_base, capacity, line_no, start, len);
+                     line_base, staging_cap, capacity, line_no, start, len);
+  return hipGetLastError();
+}
+
+hipError_t verify_candidates(const VerifyArgs& v, hipStream_t stream) {
+  uint64_t grid = (v.ntiles + 3) / 4;
+  if (grid > 16384) grid = 16384;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(256), 0, stream, v);
   return hipGetLastError();
 }
 

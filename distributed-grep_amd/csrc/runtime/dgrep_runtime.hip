@@ -43,8 +43,9 @@ hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
 hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStream_t stream);
 uint64_t order_blocks(uint64_t ntiles);
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
-                       uint64_t* line_base, uint64_t* blk, uint64_t capacity, uint64_t* line_no, uint64_t* start,
-                       uint32_t* len, hipStream_t stream);
+                       uint64_t* line_base, uint64_t* blk, uint64_t staging_cap, uint64_t capacity,
+                       uint64_t* line_no, uint64_t* start, uint32_t* len, hipStream_t stream);
+hipError_t verify_candidates(const VerifyArgs& v, hipStream_t stream);
 }  // namespace dgrep
 
 using namespace dgrep;
@@ -69,13 +70,18 @@ struct dgrep_ctx {
   uint32_t table_bytes = 0;
   uint16_t* d_wide = nullptr;  // kStepWide: the whole u16 [state][class] table
   uint32_t nclasses = 0, hot_entries = 0;
-  // dgrep_set_stepper: force a stepper (0 auto, 1 wide, 2 u8 table, 3 pair) /
+  // dgrep_set_stepper: force a stepper (0 auto, 1 wide, 2 u8 table, 3 pair, 4 filter) /
   // cap the wide stepper's LDS rows (tests, tuning)
   int force_stepper = 0;
   uint32_t wide_hot_rows_cap = UINT32_MAX;
   uint32_t lane_chunk = 0;  // dgrep_set_lane_chunk (0 = adaptive)
   int step_kind = kStepTable;
   PairArgs pair_args;
+  // kStepFilter: CAND_END (premultiplied), and the whole DFA for verify_kernel
+  uint32_t cand_end = UINT32_MAX;
+  uint16_t* d_full = nullptr;  // u16 [nstates][nclasses], the blob's ids
+  uint8_t* d_cls = nullptr;    // [256]
+  uint32_t blob_start = 0, blob_start_m = 0;
   int blocks_per_cu = 1;
 
   // per-scan scratch (grown on demand, reused)
@@ -99,7 +105,8 @@ struct dgrep_ctx {
   uint32_t* d_res_len = nullptr;
   uint64_t res_cap = 0;
 
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr;
+  uint64_t staged_hint = 0;  // kStepFilter: staged lines (candidates included) of the last scan
   float last_ms = 0.f;
   dgrep_scan_stats stats{};
   // matching lines per byte of the last scan of the loaded pattern (0 after
@@ -233,6 +240,59 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   return true;
 }
 
+// The filter stepper's LDS image (StepFilter, scan_dfa.hip): the DFA's first
+// R - 2 states in breadth-first order from start (start_m at depth 0), as many
+// rows as kFilterImageBytes holds, plus CAND (every transition out of them;
+// '\n' -> CAND_END) and CAND_END (start's row). Ids: kept states other than
+// start_m, CAND, start_m, CAND_END; entries premultiplied by K. Returns false
+// if not even start, start_m and their successors fit.
+bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint32_t row_cap, std::vector<uint8_t>* img,
+                        uint32_t* start, uint32_t* start_m, uint32_t* cand_end) {
+  const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
+  const uint32_t cn = h.byte_class[uint8_t('\n')];
+  // rows that fit (row_cap: dgrep_set_stepper's test knob)
+  const uint32_t R = std::min<uint32_t>((kFilterImageBytes - kWideClassBytes) / (2 * K), row_cap);
+  if (R < 4 || uint64_t(R) * K > 65535) return false;
+  std::vector<uint32_t> order;
+  std::vector<uint8_t> seen(S, 0);
+  auto visit = [&](uint32_t x) {
+    if (!seen[x]) { seen[x] = 1; order.push_back(x); }
+  };
+  visit(h.start);
+  visit(M);
+  for (size_t q = 0; q < order.size(); ++q)
+    for (uint32_t k = 0; k < K; ++k) visit(trans[size_t(order[q]) * K + k]);
+  const uint32_t keep = std::min<uint32_t>(uint32_t(order.size()), S <= R ? S : R - 2);
+  if (keep < 2) return false;
+  std::vector<uint32_t> id(S, UINT32_MAX);
+  uint32_t next = 0;
+  for (uint32_t i = 0; i < keep; ++i)
+    if (order[i] != M) id[order[i]] = next++;
+  const bool exact = keep == S;  // the whole DFA fits: no candidates
+  const uint32_t CAND = exact ? UINT32_MAX : next++;
+  id[M] = next++;
+  const uint32_t CEND = exact ? UINT32_MAX : next++;
+  const uint32_t Sf = next;
+  auto to = [&](uint32_t x) { return uint16_t((id[x] == UINT32_MAX ? CAND : id[x]) * K); };
+  img->assign((kWideClassBytes + size_t(Sf) * K * 2 + 15) & ~size_t(15), 0);
+  memcpy(img->data(), h.byte_class, 256);
+  uint16_t* rows = reinterpret_cast<uint16_t*>(img->data() + kWideClassBytes);
+  for (uint32_t i = 0; i < keep; ++i) {
+    const uint32_t x = order[i];
+    for (uint32_t k = 0; k < K; ++k) rows[size_t(id[x]) * K + k] = to(trans[size_t(x) * K + k]);
+  }
+  if (!exact) {
+    for (uint32_t k = 0; k < K; ++k) {
+      rows[size_t(CAND) * K + k] = uint16_t((k == cn ? CEND : CAND) * K);
+      rows[size_t(CEND) * K + k] = to(trans[size_t(h.start) * K + k]);
+    }
+  }
+  *start = id[h.start] * K;
+  *start_m = id[M] * K;
+  *cand_end = exact ? UINT32_MAX : CEND * K;
+  return true;
+}
+
 }  // namespace
 
 extern "C" int dgrep_open(int device, dgrep_ctx** out) {
@@ -247,6 +307,8 @@ extern "C" int dgrep_open(int device, dgrep_ctx** out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipEventCreate(&c->ev2);
   if (e == hipSuccess) e = hipEventCreate(&c->ev3);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev4);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev5);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), 4 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     // keep the context so the caller can read the message
@@ -263,7 +325,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_cls, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -278,6 +340,8 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev2) (void)hipEventDestroy(c->ev2);
   if (c->ev3) (void)hipEventDestroy(c->ev3);
+  if (c->ev4) (void)hipEventDestroy(c->ev4);
+  if (c->ev5) (void)hipEventDestroy(c->ev5);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -301,7 +365,7 @@ extern "C" int dgrep_set_lane_chunk(dgrep_ctx* c, uint32_t chunk_bytes) {
 }
 
 extern "C" int dgrep_set_stepper(dgrep_ctx* c, int force, uint32_t wide_hot_rows) {
-  if (!c || force < 0 || force > 3) return DGREP_E_INVALID;
+  if (!c || force < 0 || force > 4) return DGREP_E_INVALID;
   c->force_stepper = force;
   c->wide_hot_rows_cap = wide_hot_rows ? wide_hot_rows : UINT32_MAX;
   return DGREP_OK;
@@ -342,12 +406,38 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     c->err = "dgrep_load_dfa: the pair stepper's two-byte table does not fit this DFA";
     return DGREP_E_UNSUPPORTED;
   }
+  std::vector<uint8_t> filter_img;
+  uint32_t f_start = 0, f_m = 0, f_cend = UINT32_MAX;
+  const bool filter_ok = !pair_ok && ((force == 0 && h.nstates > 256) || force == 4) &&
+                         build_filter_image(h, trans, c->wide_hot_rows_cap, &filter_img, &f_start, &f_m, &f_cend);
+  if (force == 4 && !filter_ok) {
+    c->err = "dgrep_load_dfa: the filter stepper cannot hold this DFA's first states";
+    return DGREP_E_UNSUPPORTED;
+  }
   if (pair_ok) {
     c->step_kind = kStepPair;
     c->nclasses = h.nclasses;
     t.swap(pair_img);
     start = pair_start;
     start_m = pair_m;
+  } else if (filter_ok) {
+    c->step_kind = kStepFilter;
+    c->nclasses = h.nclasses;
+    c->cand_end = f_cend;
+    t.swap(filter_img);
+    start = f_start;
+    start_m = f_m;
+    // the whole DFA (blob ids) for verify_kernel
+    std::vector<uint16_t> full(size_t(h.nstates) * h.nclasses);
+    for (size_t i = 0; i < full.size(); ++i) full[i] = uint16_t(trans[i]);
+    if (c->d_full) HIPCHK(hipFree(c->d_full));
+    c->d_full = nullptr;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_full), full.size() * 2));
+    HIPCHK(hipMemcpy(c->d_full, full.data(), full.size() * 2, hipMemcpyHostToDevice));
+    if (!c->d_cls) HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_cls), 256));
+    HIPCHK(hipMemcpy(c->d_cls, h.byte_class, 256, hipMemcpyHostToDevice));
+    c->blob_start = h.start;
+    c->blob_start_m = h.start_m;
   } else if (h.nstates > 256 || force == 1) {
     // StepWide: renumber hottest-first -- start, start_m, then breadth-first
     // from start -- so the shallow states sit in the LDS-resident rows
@@ -420,6 +510,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   HIPCHK(scan_dfa_occupancy(c->step_kind, c->table_bytes, &bpc));
   c->blocks_per_cu = std::max(1, bpc);
   c->density = 0.0;
+  c->staged_hint = 0;
   c->loaded = true;
   return DGREP_OK;
 }
@@ -463,7 +554,11 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   if ((rc = grow(c, &c->d_out_off, &c->off_cap, ntiles + 1)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_line_base, &c->lb_cap, ntiles + 1)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_blk, &c->blk_cap, 2 * order_blocks(ntiles) + 2)) != DGREP_OK) return rc;
-  if ((rc = grow(c, &c->d_staging, &c->staging_cap, capacity)) != DGREP_OK) return rc;
+  // kStepFilter stages its candidates too: the staging buffer holds at least
+  // the previous scan's staged lines, and grows (one re-scan) if they overflow
+  const bool filt = c->step_kind == kStepFilter && c->cand_end != UINT32_MAX;
+  if ((rc = grow(c, &c->d_staging, &c->staging_cap, filt ? std::max(capacity, c->staged_hint) : capacity)) != DGREP_OK)
+    return rc;
 
   if (!c->d_overflow && (rc = grow(c, &c->d_overflow, &c->overflow_cap, 1u << 16)) != DGREP_OK) return rc;
 
@@ -477,8 +572,6 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.start_m = c->start_m;
   a.chunk = chunk;
   a.ntiles = ntiles;
-  a.staging = c->d_staging;
-  a.capacity = capacity;
   a.counter = c->d_counters;
   a.tiles = c->d_tiles;
   a.status = reinterpret_cast<uint32_t*>(c->d_counters + 2);
@@ -489,6 +582,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.pair_t1 = c->pair_args.t1;
   a.pair_thr = c->pair_args.thr;
   a.pair_div = c->pair_args.div;
+  a.cand_end = c->cand_end;
   // every resident workgroup is launched even when the last round of tiles is
   // part-empty: trimming the grid so that every wave runs the same number of
   // tiles leaves some CUs with 2 workgroups and others with 3, and the time
@@ -499,7 +593,9 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   S.lane_chunk = chunk;
   S.lane_slots = slots;
   S.tiles = ntiles;
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    a.staging = c->d_staging;
+    a.capacity = c->staging_cap;
     a.overflow = c->d_overflow;
     a.overflow_cap = c->overflow_cap;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
@@ -512,29 +608,66 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     S.scan_ms += ms;  // a re-run scan is counted: it is part of this call's device time
     ++S.scan_attempts;
-    if (ctr[1] <= c->overflow_cap) break;
-    // more overflowing lanes than recorded: grow the list and scan again
-    if ((rc = grow(c, &c->d_overflow, &c->overflow_cap, ctr[1])) != DGREP_OK) return rc;
+    if (ctr[1] > c->overflow_cap) {
+      // more overflowing lanes than recorded: grow the list and scan again
+      if ((rc = grow(c, &c->d_overflow, &c->overflow_cap, ctr[1])) != DGREP_OK) return rc;
+    } else if (filt && ctr[0] > c->staging_cap) {
+      // candidates included, more staged lines than the staging buffer holds
+      if ((rc = grow(c, &c->d_staging, &c->staging_cap, ctr[0] + ctr[0] / 8)) != DGREP_OK) return rc;
+    } else {
+      break;
+    }
   }
-  const uint64_t total = ctr[0];
+  const uint64_t staged = ctr[0];
   S.overflow_lanes = ctr[1];
-  S.matches = total;
   c->last_ms = S.scan_ms;
   if (uint32_t(ctr[2]) & kStatusLineTooLong) {
     c->err = "a matching line is longer than 4 GiB (uint32 length in dgrep_result)";
     return DGREP_E_UNSUPPORTED;
   }
-  c->density = double(total) / double(n);
-  const bool over = ctr[1] && total <= capacity;
+  if (uint32_t(ctr[2]) & kStatusCandidateTooLong) {
+    c->err = "a line that leaves the filter's LDS-resident states is longer than 2 GiB";
+    return DGREP_E_UNSUPPORTED;
+  }
+  // matching (and candidate) lines per byte: caps the next scan's lane chunk
+  c->density = double(staged) / double(n);
+  const bool over = ctr[1] && staged <= a.capacity;
   if (over) {
     HIPCHK(hipEventRecord(c->ev2, c->stream));
     HIPCHK(scan_dfa_overflow(c->step_kind, a, ctr[1], c->stream));
     HIPCHK(hipEventRecord(c->ev3, c->stream));
   }
+  uint64_t total = staged;
+  if (filt && staged && staged <= a.capacity) {
+    VerifyArgs v;
+    v.data = d_data;
+    v.full = c->d_full;
+    v.cls = c->d_cls;
+    v.nclasses = c->nclasses;
+    v.start = c->blob_start;
+    v.start_m = c->blob_start_m;
+    v.tiles = c->d_tiles;
+    v.ntiles = ntiles;
+    v.staging = c->d_staging;
+    v.staging_cap = c->staging_cap;
+    v.removed = c->d_counters + 3;  // zeroed before the scan
+    HIPCHK(hipEventRecord(c->ev4, c->stream));
+    HIPCHK(verify_candidates(v, c->stream));
+    HIPCHK(hipEventRecord(c->ev5, c->stream));
+    unsigned long long removed = 0;
+    HIPCHK(hipMemcpyAsync(&removed, c->d_counters + 3, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventElapsedTime(&S.verify_ms, c->ev4, c->ev5));
+    c->last_ms += S.verify_ms;
+    total = staged - removed;
+    S.candidates = removed;  // dropped ones; kept candidates count as matches
+  }
+  if (filt) c->staged_hint = staged;
+  S.matches = total;
   *count = total;
   if (total != 0 && total <= capacity)
-    HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->d_blk, capacity, d_line,
-                       d_start, d_len, c->stream));
+    HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->d_blk, c->staging_cap,
+                       capacity, d_line, d_start, d_len, c->stream));
   if (over || (total != 0 && total <= capacity)) HIPCHK(hipStreamSynchronize(c->stream));
   if (over) {
     HIPCHK(hipEventElapsedTime(&S.overflow_ms, c->ev2, c->ev3));

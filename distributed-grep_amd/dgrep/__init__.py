@@ -56,7 +56,7 @@ EXPORTS = (
     "dgrep_reduce", "dgrep_reduce_free", "dgrep_last_scan_stats", "dgrep_build_info",
 )
 
-STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair"}
+STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair", 4: "filter"}
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
 
@@ -88,7 +88,8 @@ class _ReduceOut(ctypes.Structure):
 class _ScanStats(ctypes.Structure):
     _fields_ = [("stepper", ctypes.c_uint32), ("lane_chunk", ctypes.c_uint32), ("lane_slots", ctypes.c_uint32),
                 ("scan_attempts", ctypes.c_uint32), ("tiles", ctypes.c_uint64), ("overflow_lanes", ctypes.c_uint64),
-                ("matches", ctypes.c_uint64), ("scan_ms", ctypes.c_float), ("overflow_ms", ctypes.c_float)]
+                ("matches", ctypes.c_uint64), ("scan_ms", ctypes.c_float), ("overflow_ms", ctypes.c_float),
+                ("verify_ms", ctypes.c_float), ("candidates", ctypes.c_uint64)]
 
 
 class _BlobInfo(ctypes.Structure):
@@ -254,12 +255,12 @@ class Context:
         (dgrep_set_lane_chunk; 0 = adaptive)."""
         self._check(self._L.dgrep_set_lane_chunk(self._h, chunk_bytes))
 
-    _FORCE = {"auto": 0, "wide": 1, "table": 2, "pair": 3}
+    _FORCE = {"auto": 0, "wide": 1, "table": 2, "pair": 3, "filter": 4}
 
     def set_stepper(self, force=False, wide_hot_rows: int = 0):
         """Testing/tuning: the stepper the next load() uses (dgrep_set_stepper):
         "auto" (default: by DFA size), "wide", "table" (u8, <= 256 states) or
-        "pair" (fails at load if its two-byte table does not fit); True/False
+        "pair" (fails at load if its two-byte table does not fit), "filter"; True/False
         mean "wide"/"auto". wide_hot_rows caps the wide stepper's LDS rows."""
         mode = self._FORCE[force] if isinstance(force, str) else int(bool(force))
         self._check(self._L.dgrep_set_stepper(self._h, mode, wide_hot_rows))

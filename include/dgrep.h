@@ -93,11 +93,14 @@ int dgrep_set_stream(dgrep_ctx* ctx, void* hip_stream);
 int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
 /* Stepper selection for later dgrep_load_dfa calls (tests / tuning only; the
  * default picks by size: <= 8 states Sheng; else the pair stepper if its
- * two-byte table fits in LDS; else <= 256 states the u8 table; else wide).
+ * two-byte table fits in LDS; else <= 256 states the u8 table; else the
+ * filter: the DFA's shallowest states in LDS, lines that leave them verified
+ * on the whole DFA).
  * force: 0 = that default, 1 = wide (u16, LDS-hot + HBM) for any DFA, 2 = the
  * u8 table (<= 256 states), 3 = pair (dgrep_load_dfa fails with
- * DGREP_E_UNSUPPORTED if it does not fit). wide_hot_rows != 0 caps the wide
- * stepper's LDS-resident rows. */
+ * DGREP_E_UNSUPPORTED if it does not fit), 4 = filter (the default above 256
+ * states). wide_hot_rows != 0 caps the LDS-resident rows of the wide stepper
+ * and of the filter (whose cut then sends nearly every line to verification). */
 int dgrep_set_stepper(dgrep_ctx* ctx, int force, uint32_t wide_hot_rows);
 /* Tests / tuning: lane chunk of the Sheng (<= 8-state) and pair steppers for
  * later scans. 0 (default) = adaptive: the compiled 4 KiB chunk, doubled (up
@@ -196,7 +199,8 @@ int dgrep_last_kernel_ms(dgrep_ctx* ctx, float* ms);
 
 /* What the last dgrep_scan* call did (tests, tuning, bench reports). */
 typedef struct {
-  uint32_t stepper;        /* 0 u8 table, 1 Sheng (<= 8 states), 2 wide u16 table, 3 pair (two bytes per lookup) */
+  uint32_t stepper;        /* 0 u8 table, 1 Sheng (<= 8 states), 2 wide u16 table, 3 pair (two bytes per lookup),
+                              4 filter (shallow DFA states in LDS + candidate verification) */
   uint32_t lane_chunk;     /* bytes per lane chunk */
   uint32_t lane_slots;     /* LDS slots per lane chunk for matching lines */
   uint32_t scan_attempts;  /* scan launches (2 if the overflow list had to grow) */
@@ -205,6 +209,8 @@ typedef struct {
   uint64_t matches;        /* matching lines */
   float scan_ms;           /* scan kernel, all attempts */
   float overflow_ms;       /* overflow pass */
+  float verify_ms;         /* filter stepper: re-run of the candidate lines on the whole DFA */
+  uint64_t candidates;     /* filter stepper: candidate lines dropped by that re-run */
 } dgrep_scan_stats;
 int dgrep_last_scan_stats(dgrep_ctx* ctx, dgrep_scan_stats* out);
 

@@ -386,9 +386,10 @@ def test_wide_stepper_boundaries_and_overflow(wide_ctx):
     _check(wide_ctx, b"error", data)
 
 
-@pytest.mark.parametrize("nkw,size", [(200, 4 << 20), (1000, 1 << 20)])
+@pytest.mark.parametrize("nkw,size", [(200, 4 << 20), (1000, 1 << 20), (1000, 12 << 20)])
 def test_keyword_alternation_c4(gpu_ctx, nkw, size):
-    """SURVEY config 4: (?i) alternation of seeded keywords (> 256 DFA states)."""
+    """SURVEY config 4: (?i) alternation of seeded keywords (> 256 DFA states):
+    the filter stepper, whose candidates are verified on the whole DFA."""
     import dgrep
 
     kws = dgrep.synth_keywords(4, nkw)
@@ -398,6 +399,55 @@ def test_keyword_alternation_c4(gpu_ctx, nkw, size):
     data = dgrep.synth_corpus_host(size, 4, 1)
     n = _check(gpu_ctx, cp, data, threads=16)
     assert n > 0
+    st = gpu_ctx.scan_stats()
+    assert st["stepper"] == ("filter" if nkw == 1000 else "filter"), st
+    if nkw == 1000:
+        assert st["candidates"] > 0, st  # lines that left the LDS states and did not match
+
+
+@pytest.fixture
+def filter_ctx(gpu_ctx):
+    yield gpu_ctx
+    gpu_ctx.set_stepper("auto")
+
+
+@pytest.mark.parametrize("rows", [0, 3, 6])  # 0: as many LDS rows as fit; 3/6: nearly every line a candidate
+@pytest.mark.parametrize("pattern", PATTERNS)
+def test_filter_stepper_forced(filter_ctx, pattern, rows):
+    filter_ctx.set_stepper("filter", rows)
+    rnd = random.Random(hash(pattern) & 0xfff)
+    alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\xe2\x82\xac", b"\xff",
+             b"WARN", b"ERROR", b"error", b"2024-01", b"key "]
+    for n in (0, 1, 100, 5000, 70000, 300000):
+        data = b"".join(rnd.choice(alpha) for _ in range(n // 3))
+        try:
+            _check(filter_ctx, pattern, data)
+        except dgrep_unsupported():
+            assert rows in (3, 6)  # too few rows for start, start_m and CAND
+            return
+        if n:
+            assert filter_ctx.scan_stats()["stepper"] == "filter"
+
+
+def dgrep_unsupported():
+    import dgrep
+
+    return dgrep.UnsupportedPattern
+
+
+def test_filter_candidates_dense_and_long(filter_ctx):
+    """Every line a candidate (3 LDS rows): staging grows past the caller's
+    capacity, verification keeps exactly the matching lines, at chunk, tile
+    and overflow edges; lines longer than a chunk."""
+    import dgrep
+
+    filter_ctx.set_stepper("filter", 4)
+    for pattern in (b"error", b"(WARN|ERROR) [a-z_]+", b"^$|ab x"):
+        for data in (_dense_lines(5, 60000, 6), _dense_lines(6, 3000, 3000),
+                     dgrep.synth_corpus_host(3 << 20, 9, 0)):
+            _check(filter_ctx, pattern, data, threads=16)
+            st = filter_ctx.scan_stats()
+            assert st["stepper"] == "filter", st
 
 
 # ---- the pair stepper (two bytes per LDS lookup, shadow states) -------------
@@ -431,9 +481,10 @@ def test_pair_stepper_edges_and_random(pair_ctx, pattern):
 
 
 @pytest.mark.parametrize("chunk", [4096, 8192, 32768])
-def test_pair_stepper_chunk_and_tile_edges(gpu_ctx, chunk):
+def test_pair_stepper_chunk_and_tile_edges(pair_ctx, chunk):
     import dgrep
 
+    gpu_ctx = pair_ctx
     tile = 64 * chunk
     try:
         gpu_ctx.set_lane_chunk(chunk)
@@ -456,7 +507,8 @@ def test_pair_stepper_chunk_and_tile_edges(gpu_ctx, chunk):
         gpu_ctx.set_lane_chunk(0)
 
 
-def test_pair_stepper_dense_overflow(gpu_ctx):
+def test_pair_stepper_dense_overflow(pair_ctx):
+    gpu_ctx = pair_ctx
     for maxlen in (2, 5, 40, 700):
         data = _dense_lines(maxlen + 1, 40000 if maxlen < 100 else 6000, maxlen)
         for pattern in (b"(WARN|ERROR) [a-z_]+", b"^$|error", b"b x*$"):
