@@ -63,7 +63,8 @@ struct ScanArgs {
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids
 struct VerifyArgs {
   const uint8_t* data;
-  const uint16_t* full;  // u16 [nstates][nclasses], HBM
+  const void* full;      // [nstates][nclasses], HBM: u16 entries, or u32 if full_u32
+  uint32_t full_u32;
   const uint8_t* cls;    // [256] byte classes, HBM
   uint32_t nclasses, start, start_m;
   TileInfo* tiles;

@@ -1107,8 +1107,8 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
 
 // ---- filter verification (kStepFilter) -------------------------------------
 // One wave per tile: every candidate line (kCandidateBit) of the tile's staged
-// lines is re-run from its start on the WHOLE DFA (u16 [state][class] in HBM,
-// L2-resident; classes in LDS) and kept iff the '\n' after it enters start_m
+// lines is re-run from its start on the WHOLE DFA ([state][class] in HBM, u16
+// or, above 65535 states, u32; L2/MALL-resident; classes in LDS) and kept iff the '\n' after it enters start_m
 // (grep.go:21 on that line); the tile's kept lines are compacted in place, in
 // order, and its count updated; `removed` receives the dropped candidates.
 __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
@@ -1118,7 +1118,11 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t waves = uint64_t(gridDim.x) * 4;
   const uint32_t K = v.nclasses, cn = cls['\n'];
-  const __attribute__((address_space(1))) uint16_t* full = (const __attribute__((address_space(1))) uint16_t*)v.full;
+  const __attribute__((address_space(1))) uint16_t* full16 = (const __attribute__((address_space(1))) uint16_t*)v.full;
+  const __attribute__((address_space(1))) uint32_t* full32 = (const __attribute__((address_space(1))) uint32_t*)v.full;
+  auto next = [&](uint32_t s, uint32_t c) -> uint32_t {
+    return v.full_u32 ? full32[size_t(s) * K + c] : uint32_t(full16[size_t(s) * K + c]);
+  };
   for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
     const TileInfo ti = v.tiles[t];
     if (ti.count == 0) continue;
@@ -1135,8 +1139,8 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
           L.len &= ~kCandidateBit;
           const uint8_t* p = v.data + L.start;
           uint32_t st = v.start;
-          for (uint32_t i = 0; i < L.len; ++i) st = full[st * K + cls[p[i]]];
-          keep = full[st * K + cn] == v.start_m;
+          for (uint32_t i = 0; i < L.len; ++i) st = next(st, cls[p[i]]);
+          keep = next(st, cn) == v.start_m;
         }
       }
       const uint64_t m = __ballot(keep);
@@ -1308,9 +1312,10 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
 // slots pack a line's chunk-relative start (<= C) and '\n' index (<= C) in 16
 // bits each, so 32,768 is also the hard limit (65,536 fails GPU parity).
 // `dens_cap` (0 = none) is the largest chunk whose expected matching lines,
-// at the match density of the previous scan of this pattern, fill at most half
-// of a lane's LDS slots: a denser pattern keeps smaller chunks instead of
-// sending most lanes through the overflow pass.
+// at the match density of the previous scan of this pattern, fill at most a
+// quarter of a lane's LDS slots: a denser pattern keeps smaller chunks instead
+// of sending many lanes through the overflow pass (C4 at 16 KiB: 0.8 % of the
+// lanes overflow and the pass costs 8 % of the scan; at 8 KiB 0.07 %).
 constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
 uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c, uint64_t dens_cap) {
   uint64_t c = floor_c;
@@ -1330,7 +1335,9 @@ struct TileOp {
   hipError_t run() const {
     uint64_t c = uint64_t(Tune<S>::C);
     *slots = uint32_t(Tune<S>::E);
-    const uint64_t dens_cap = density > 0 ? uint64_t(double(Tune<S>::E) / (2.0 * density)) : 0;
+    // at most a quarter of the slots expected in use: an overflowing lane costs
+    // two latency-bound passes of the overflow kernel over its chunk
+    const uint64_t dens_cap = density > 0 ? uint64_t(double(Tune<S>::E) / (4.0 * density)) : 0;
     if constexpr (adaptive_chunk<S, T>())
       c = force ? uint64_t(force)
                 : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap);

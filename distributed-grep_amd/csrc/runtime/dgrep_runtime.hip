@@ -79,7 +79,8 @@ struct dgrep_ctx {
   PairArgs pair_args;
   // kStepFilter: CAND_END (premultiplied), and the whole DFA for verify_kernel
   uint32_t cand_end = UINT32_MAX;
-  uint16_t* d_full = nullptr;  // u16 [nstates][nclasses], the blob's ids
+  void* d_full = nullptr;      // [nstates][nclasses], the blob's ids: u16, or u32 above 65535 states
+  bool full_u32 = false;
   uint8_t* d_cls = nullptr;    // [256]
   uint32_t blob_start = 0, blob_start_m = 0;
   int blocks_per_cu = 1;
@@ -387,11 +388,6 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
       c->err = "dgrep_load_dfa: transition out of range";
       return DGREP_E_INVALID;
     }
-  if (h.nstates > 65535) {
-    c->err = "dgrep_load_dfa: DFA has " + std::to_string(h.nstates) +
-             " states; the wide stepper indexes states with u16 (at most 65535)";
-    return DGREP_E_UNSUPPORTED;
-  }
   // expand byte classes into the kernel's LDS image
   std::vector<uint8_t> t;
   std::vector<uint16_t> wide;
@@ -427,18 +423,31 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     t.swap(filter_img);
     start = f_start;
     start_m = f_m;
-    // the whole DFA (blob ids) for verify_kernel
-    std::vector<uint16_t> full(size_t(h.nstates) * h.nclasses);
-    for (size_t i = 0; i < full.size(); ++i) full[i] = uint16_t(trans[i]);
+    // the whole DFA (blob ids) for verify_kernel: u16 entries while the ids
+    // fit, u32 above 65535 states (up to the compiler's budget)
+    const size_t ne = size_t(h.nstates) * h.nclasses;
+    c->full_u32 = h.nstates > 65535;
     if (c->d_full) HIPCHK(hipFree(c->d_full));
     c->d_full = nullptr;
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_full), full.size() * 2));
-    HIPCHK(hipMemcpy(c->d_full, full.data(), full.size() * 2, hipMemcpyHostToDevice));
+    if (c->full_u32) {
+      HIPCHK(hipMalloc(&c->d_full, ne * 4));
+      HIPCHK(hipMemcpy(c->d_full, trans, ne * 4, hipMemcpyHostToDevice));
+    } else {
+      std::vector<uint16_t> full(ne);
+      for (size_t i = 0; i < ne; ++i) full[i] = uint16_t(trans[i]);
+      HIPCHK(hipMalloc(&c->d_full, ne * 2));
+      HIPCHK(hipMemcpy(c->d_full, full.data(), ne * 2, hipMemcpyHostToDevice));
+    }
     if (!c->d_cls) HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_cls), 256));
     HIPCHK(hipMemcpy(c->d_cls, h.byte_class, 256, hipMemcpyHostToDevice));
     c->blob_start = h.start;
     c->blob_start_m = h.start_m;
   } else if (h.nstates > 256 || force == 1) {
+    if (h.nstates > 65535) {
+      c->err = "dgrep_load_dfa: DFA has " + std::to_string(h.nstates) +
+               " states; the wide stepper indexes states with u16 (at most 65535)";
+      return DGREP_E_UNSUPPORTED;
+    }
     // StepWide: renumber hottest-first -- start, start_m, then breadth-first
     // from start -- so the shallow states sit in the LDS-resident rows
     c->step_kind = kStepWide;
@@ -642,6 +651,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     VerifyArgs v;
     v.data = d_data;
     v.full = c->d_full;
+    v.full_u32 = c->full_u32 ? 1u : 0u;
     v.cls = c->d_cls;
     v.nclasses = c->nclasses;
     v.start = c->blob_start;

@@ -105,7 +105,7 @@ int dgrep_set_stepper(dgrep_ctx* ctx, int force, uint32_t wide_hot_rows);
 /* Tests / tuning: lane chunk of the Sheng (<= 8-state) and pair steppers for
  * later scans. 0 (default) = adaptive: the compiled 4 KiB chunk, doubled (up
  * to 32 KiB) while every resident wave still gets a tile and the matching
- * lines the previous scan's density predicts fill at most half of a lane's
+ * lines the previous scan's density predicts fill at most a quarter of a lane's
  * LDS slots; otherwise a multiple of 128 in [4096, 32768] (LDS slots hold
  * 16-bit chunk offsets). No effect on the u8 table and wide steppers. */
 int dgrep_set_lane_chunk(dgrep_ctx* ctx, uint32_t chunk_bytes);

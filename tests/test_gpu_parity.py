@@ -533,3 +533,22 @@ def test_forced_steppers_agree_on_c3(gpu_ctx, mode):
         assert gpu_ctx.scan_stats()["stepper"] == mode
     finally:
         gpu_ctx.set_stepper("auto")
+
+
+@pytest.mark.parametrize("pattern", [b"a[ab]{15}$", b"a[ab]{16}$", b"(?i)b[ab]{14}[^b]$"])
+def test_dfa_beyond_65535_states(gpu_ctx, pattern):
+    """DFAs of 65,536 .. 2^21 states (the compiler's budget): the filter keeps
+    the shallowest rows in LDS and verifies candidate lines on the whole DFA,
+    read with u32 ids from HBM (no u16 limit)."""
+    cp = gpu_ctx.load(pattern)
+    assert cp.nstates > 65535, cp.nstates
+    rnd = random.Random(len(pattern))
+    lines = []
+    for _ in range(30000):
+        L = rnd.choice([3, 10, 17, 18, 25, 60])
+        lines.append(bytes(rnd.choice(b"abAB") if rnd.random() < 0.97 else rnd.choice(b"x \xc5") for _ in range(L)))
+    data = b"\n".join(lines)
+    n = _check(gpu_ctx, cp, data, threads=16)
+    assert n > 0
+    st = gpu_ctx.scan_stats()
+    assert st["stepper"] == "filter" and st["candidates"] > 0, st
