@@ -63,8 +63,9 @@ struct ScanArgs {
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids
 struct VerifyArgs {
   const uint8_t* data;
-  const void* full;      // [nstates][nclasses], HBM: u16 entries, or u32 if full_u32
+  const void* full;      // [nstates][nclasses] breadth-first ids, HBM: u16 entries, or u32 if full_u32
   uint32_t full_u32;
+  uint32_t hot_entries;  // leading entries of `full` verify_kernel copies to LDS
   const uint8_t* cls;    // [256] byte classes, HBM
   uint32_t nclasses, start, start_m;
   TileInfo* tiles;
@@ -92,7 +93,7 @@ enum : int {
   kStepFilter = 4,  // > 256 states: the DFA's shallow part in LDS, lines that leave it verified afterwards
 };
 
-// LDS image of kStepFilter: 256 class bytes, then u16 [state][class] rows of the
+// LDS image of kStepFilter: u32 classes [256], then u16 [state][class] rows of the
 // filter DFA (its states premultiplied by the class count), at most this many
 // bytes in all -- with 1024 threads x 4 slots x 8 B the workgroup stays within
 // the CU's 160 KiB.
@@ -100,6 +101,7 @@ enum : int {
 #define DGREP_FILTER_KIB 124
 #endif
 constexpr uint32_t kFilterImageBytes = DGREP_FILTER_KIB * 1024;
+constexpr uint32_t kFilterClassBytes = 1024;
 
 // StepPair's two-byte table T2 (u16 [state][class][class], premultiplied
 // states) must address itself with 16-bit values; its whole LDS image (T2 +

@@ -341,11 +341,13 @@ struct StepPair {
 // that does is emitted as a CANDIDATE (kCandidateBit) and verify_kernel re-runs
 // it on the whole DFA. For C4's 1,000 keywords the shallow part is depth <= 3
 // of the Aho-Corasick-like DFA and 0.8 % of the lines are candidates.
-// LDS: 256 class bytes, then u16 [state][class] rows, entries premultiplied by
-// the class count (entry index of the next state's row): the dependent chain
-// per byte is one v_add_lshl + one ds_read_u16; the class lookups depend only on
-// the input and are issued a word ahead. Ids: shallow states, CAND, start_m,
-// CAND_END -- an event is a state >= start_m.
+// LDS: the byte classes as u32 [256] (byte b in bank b % 32: text bytes spread
+// over the banks, where u8 entries would pile the letters into 7 banks), then
+// u16 [state][class] rows, entries premultiplied by the class count (entry
+// index of the next state's row): the dependent chain per byte is one
+// v_add_lshl + one ds_read_u16; the class lookups depend only on the input and
+// are issued a word ahead. Ids: shallow states, CAND, start_m, CAND_END -- an
+// event is a state >= start_m.
 struct StepFilter {
   static constexpr int kKind = kStepFilter;
   const uint8_t* lds;
@@ -353,11 +355,12 @@ struct StepFilter {
   struct Pre {
     uint32_t c0, c1, c2, c3;
   };
+  __device__ __forceinline__ uint32_t cls(uint32_t b) const { return *reinterpret_cast<const uint32_t*>(lds + 4u * b); }
   __device__ __forceinline__ Pre prep(uint32_t x) const {
-    return Pre{lds[x & 0xffu], lds[(x >> 8) & 0xffu], lds[(x >> 16) & 0xffu], lds[x >> 24]};
+    return Pre{cls(x & 0xffu), cls((x >> 8) & 0xffu), cls((x >> 16) & 0xffu), cls(x >> 24)};
   }
   __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t c) const {
-    return *reinterpret_cast<const uint16_t*>(lds + kWideClassBytes + 2u * (s + c));
+    return *reinterpret_cast<const uint16_t*>(lds + kFilterClassBytes + 2u * (s + c));
   }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
@@ -366,7 +369,7 @@ struct StepFilter {
     s2 = one(s1, p.c2);
     s3 = one(s2, p.c3);
   }
-  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return one(s, lds[b]); }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return one(s, cls(b)); }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s >= M; }
 };
 
@@ -1107,21 +1110,31 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
 
 // ---- filter verification (kStepFilter) -------------------------------------
 // One wave per tile: every candidate line (kCandidateBit) of the tile's staged
-// lines is re-run from its start on the WHOLE DFA ([state][class] in HBM, u16
-// or, above 65535 states, u32; L2/MALL-resident; classes in LDS) and kept iff the '\n' after it enters start_m
-// (grep.go:21 on that line); the tile's kept lines are compacted in place, in
-// order, and its count updated; `removed` receives the dropped candidates.
+// lines is re-run from its start on the WHOLE DFA and kept iff the '\n' after
+// it enters start_m (grep.go:21 on that line); the tile's kept lines are
+// compacted in place, in order, and its count updated; `removed` receives the
+// dropped candidates. The whole DFA is numbered breadth-first from start (the
+// runtime's order), so the rows a candidate line spends most of its bytes in
+// are the first ones: kVerifyHotBytes of them are copied to LDS, the rest are
+// read from HBM (L2-resident: [state][class], u16 entries, or u32 above 65535
+// states). A line is read in aligned 16-byte pieces.
+constexpr uint32_t kVerifyHotBytes = 48 * 1024;
+template <typename E>
 __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
-  __shared__ uint8_t cls[256];
+  __shared__ uint32_t cls[256];
+  __shared__ __attribute__((aligned(16))) E hot[kVerifyHotBytes / sizeof(E)];
   cls[threadIdx.x] = v.cls[threadIdx.x];
+  const E* full = static_cast<const E*>(v.full);
+  const uint32_t hot_n = v.hot_entries;
+  for (uint32_t i = threadIdx.x; i < hot_n; i += 256) hot[i] = full[i];
   __syncthreads();
+  const __attribute__((address_space(1))) E* gfull = (const __attribute__((address_space(1))) E*)v.full;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t waves = uint64_t(gridDim.x) * 4;
   const uint32_t K = v.nclasses, cn = cls['\n'];
-  const __attribute__((address_space(1))) uint16_t* full16 = (const __attribute__((address_space(1))) uint16_t*)v.full;
-  const __attribute__((address_space(1))) uint32_t* full32 = (const __attribute__((address_space(1))) uint32_t*)v.full;
   auto next = [&](uint32_t s, uint32_t c) -> uint32_t {
-    return v.full_u32 ? full32[size_t(s) * K + c] : uint32_t(full16[size_t(s) * K + c]);
+    const size_t i = size_t(s) * K + c;
+    return i < hot_n ? uint32_t(hot[i]) : uint32_t(gfull[i]);
   };
   for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
     const TileInfo ti = v.tiles[t];
@@ -1137,9 +1150,17 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
         keep = true;
         if (L.len & kCandidateBit) {
           L.len &= ~kCandidateBit;
-          const uint8_t* p = v.data + L.start;
+          const uint64_t a = L.start, e = L.start + L.len;
           uint32_t st = v.start;
-          for (uint32_t i = 0; i < L.len; ++i) st = next(st, cls[p[i]]);
+          for (uint64_t q = a & ~uint64_t(15); q < e; q += 16) {
+            const uint4 w = *reinterpret_cast<const uint4*>(v.data + q);
+            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const uint64_t pos = q + uint64_t(j);
+              if (pos >= a && pos < e) st = next(st, cls[(ws[j >> 2] >> (8 * (j & 3))) & 0xffu]);
+            }
+          }
           keep = next(st, cn) == v.start_m;
         }
       }
@@ -1404,11 +1425,16 @@ hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_
   return hipGetLastError();
 }
 
+uint32_t verify_hot_bytes() { return kVerifyHotBytes; }
+
 hipError_t verify_candidates(const VerifyArgs& v, hipStream_t stream) {
   uint64_t grid = (v.ntiles + 3) / 4;
   if (grid > 16384) grid = 16384;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(256), 0, stream, v);
+  if (v.full_u32)
+    hipLaunchKernelGGL(verify_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, v);
+  else
+    hipLaunchKernelGGL(verify_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, v);
   return hipGetLastError();
 }
 

@@ -46,6 +46,7 @@ hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_
                        uint64_t* line_base, uint64_t* blk, uint64_t staging_cap, uint64_t capacity,
                        uint64_t* line_no, uint64_t* start, uint32_t* len, hipStream_t stream);
 hipError_t verify_candidates(const VerifyArgs& v, hipStream_t stream);
+uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
 using namespace dgrep;
@@ -82,7 +83,8 @@ struct dgrep_ctx {
   void* d_full = nullptr;      // [nstates][nclasses], the blob's ids: u16, or u32 above 65535 states
   bool full_u32 = false;
   uint8_t* d_cls = nullptr;    // [256]
-  uint32_t blob_start = 0, blob_start_m = 0;
+  uint32_t blob_start = 0, blob_start_m = 0;  // start / start_m in d_full's (breadth-first) ids
+  uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
   int blocks_per_cu = 1;
 
   // per-scan scratch (grown on demand, reused)
@@ -241,7 +243,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   return true;
 }
 
-// The filter stepper's LDS image (StepFilter, scan_dfa.hip): the DFA's first
+// The filter stepper's LDS image (StepFilter, scan_dfa.hip): u32 byte classes,
+// then u16 rows of the DFA's first
 // R - 2 states in breadth-first order from start (start_m at depth 0), as many
 // rows as kFilterImageBytes holds, plus CAND (every transition out of them;
 // '\n' -> CAND_END) and CAND_END (start's row). Ids: kept states other than
@@ -252,7 +255,7 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
   const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
   const uint32_t cn = h.byte_class[uint8_t('\n')];
   // rows that fit (row_cap: dgrep_set_stepper's test knob)
-  const uint32_t R = std::min<uint32_t>((kFilterImageBytes - kWideClassBytes) / (2 * K), row_cap);
+  const uint32_t R = std::min<uint32_t>((kFilterImageBytes - kFilterClassBytes) / (2 * K), row_cap);
   if (R < 4 || uint64_t(R) * K > 65535) return false;
   std::vector<uint32_t> order;
   std::vector<uint8_t> seen(S, 0);
@@ -275,9 +278,10 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
   const uint32_t CEND = exact ? UINT32_MAX : next++;
   const uint32_t Sf = next;
   auto to = [&](uint32_t x) { return uint16_t((id[x] == UINT32_MAX ? CAND : id[x]) * K); };
-  img->assign((kWideClassBytes + size_t(Sf) * K * 2 + 15) & ~size_t(15), 0);
-  memcpy(img->data(), h.byte_class, 256);
-  uint16_t* rows = reinterpret_cast<uint16_t*>(img->data() + kWideClassBytes);
+  img->assign((kFilterClassBytes + size_t(Sf) * K * 2 + 15) & ~size_t(15), 0);
+  uint32_t* cls = reinterpret_cast<uint32_t*>(img->data());
+  for (int b = 0; b < 256; ++b) cls[b] = h.byte_class[b];
+  uint16_t* rows = reinterpret_cast<uint16_t*>(img->data() + kFilterClassBytes);
   for (uint32_t i = 0; i < keep; ++i) {
     const uint32_t x = order[i];
     for (uint32_t k = 0; k < K; ++k) rows[size_t(id[x]) * K + k] = to(trans[size_t(x) * K + k]);
@@ -423,25 +427,39 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     t.swap(filter_img);
     start = f_start;
     start_m = f_m;
-    // the whole DFA (blob ids) for verify_kernel: u16 entries while the ids
-    // fit, u32 above 65535 states (up to the compiler's budget)
-    const size_t ne = size_t(h.nstates) * h.nclasses;
-    c->full_u32 = h.nstates > 65535;
+    // the whole DFA for verify_kernel, renumbered breadth-first from start
+    // (start, start_m, then BFS) so its hot rows lead; u16 entries while the
+    // ids fit, u32 above 65535 states (up to the compiler's budget)
+    const uint32_t S = h.nstates, K = h.nclasses;
+    std::vector<uint32_t> order, bid(S, UINT32_MAX);
+    order.reserve(S);
+    auto visit = [&](uint32_t x) {
+      if (bid[x] == UINT32_MAX) { bid[x] = uint32_t(order.size()); order.push_back(x); }
+    };
+    visit(h.start);
+    visit(h.start_m);
+    for (size_t q = 0; q < order.size(); ++q)
+      for (uint32_t k = 0; k < K; ++k) visit(trans[size_t(order[q]) * K + k]);
+    for (uint32_t x = 0; x < S; ++x) visit(x);
+    const size_t ne = size_t(S) * K;
+    c->full_u32 = S > 65535;
     if (c->d_full) HIPCHK(hipFree(c->d_full));
     c->d_full = nullptr;
-    if (c->full_u32) {
-      HIPCHK(hipMalloc(&c->d_full, ne * 4));
-      HIPCHK(hipMemcpy(c->d_full, trans, ne * 4, hipMemcpyHostToDevice));
-    } else {
-      std::vector<uint16_t> full(ne);
-      for (size_t i = 0; i < ne; ++i) full[i] = uint16_t(trans[i]);
-      HIPCHK(hipMalloc(&c->d_full, ne * 2));
-      HIPCHK(hipMemcpy(c->d_full, full.data(), ne * 2, hipMemcpyHostToDevice));
-    }
+    const size_t esz = c->full_u32 ? 4 : 2;
+    std::vector<uint8_t> full(ne * esz);
+    for (uint32_t n = 0; n < S; ++n)
+      for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t x = bid[trans[size_t(order[n]) * K + k]];
+        if (c->full_u32) reinterpret_cast<uint32_t*>(full.data())[size_t(n) * K + k] = x;
+        else reinterpret_cast<uint16_t*>(full.data())[size_t(n) * K + k] = uint16_t(x);
+      }
+    HIPCHK(hipMalloc(&c->d_full, full.size()));
+    HIPCHK(hipMemcpy(c->d_full, full.data(), full.size(), hipMemcpyHostToDevice));
+    c->verify_hot = uint32_t(std::min<size_t>(ne, verify_hot_bytes() / esz)) / K * K;
     if (!c->d_cls) HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_cls), 256));
     HIPCHK(hipMemcpy(c->d_cls, h.byte_class, 256, hipMemcpyHostToDevice));
-    c->blob_start = h.start;
-    c->blob_start_m = h.start_m;
+    c->blob_start = bid[h.start];
+    c->blob_start_m = bid[h.start_m];
   } else if (h.nstates > 256 || force == 1) {
     if (h.nstates > 65535) {
       c->err = "dgrep_load_dfa: DFA has " + std::to_string(h.nstates) +
@@ -652,6 +670,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.data = d_data;
     v.full = c->d_full;
     v.full_u32 = c->full_u32 ? 1u : 0u;
+    v.hot_entries = c->verify_hot;
     v.cls = c->d_cls;
     v.nclasses = c->nclasses;
     v.start = c->blob_start;
