@@ -546,7 +546,7 @@ def test_dfa_beyond_65535_states(gpu_ctx, pattern):
     lines = []
     for _ in range(30000):
         L = rnd.choice([3, 10, 17, 18, 25, 60])
-        lines.append(bytes(rnd.choice(b"abAB") if rnd.random() < 0.97 else rnd.choice(b"x \xc5") for _ in range(L)))
+        lines.append(bytes(rnd.choice(b"ababababAB") if rnd.random() < 0.98 else rnd.choice(b"x \xc5") for _ in range(L)))
     data = b"\n".join(lines)
     n = _check(gpu_ctx, cp, data, threads=16)
     assert n > 0
