@@ -71,23 +71,24 @@ bool in_table(const unsigned int* r, int nranges, int32_t x) {
 
 bool ascii_alnum(int32_t c) { return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'); }
 
-// [Go stdlib] unicode.SimpleFold orbit of r. Only the orbits that touch ASCII
-// letters are known offline: {X, x}, {K, k, U+212A}, {S, s, U+017F}. Returns
-// false for any other rune that takes part in case mapping.
-bool fold_orbit(int32_t r, RuneSet* out) {
-  if ((r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z')) {
-    int32_t l = r | 0x20;
-    out->add(l, l);
-    out->add(l - 0x20, l - 0x20);
-    if (l == 'k') out->add(0x212A, 0x212A);
-    if (l == 's') out->add(0x17F, 0x17F);
-    return true;
+// [Go stdlib] unicode.SimpleFold orbit of r (every rune equivalent to r under
+// simple case folding, r included): dg_fold lists, sorted by rune, the next
+// member of each orbit of two or more (tools/gen_unicode_tables.py, Unicode
+// 13.0 as in Go 1.18); a rune not listed folds only to itself.
+int fold_next(int32_t r) {
+  int lo = 0, hi = dg_nfold;
+  while (lo < hi) {
+    const int m = (lo + hi) / 2;
+    const int32_t x = int32_t(dg_fold[2 * m]);
+    if (x == r) return int32_t(dg_fold[2 * m + 1]);
+    if (x < r) lo = m + 1;
+    else hi = m;
   }
-  if (r == 0x212A) { out->add('K', 'K'); out->add('k', 'k'); out->add(r, r); return true; }
-  if (r == 0x17F) { out->add('S', 'S'); out->add('s', 's'); out->add(r, r); return true; }
-  if (r >= 0x80 && in_table(dg_cased, dg_ncased, r)) return false;
+  return -1;
+}
+void fold_orbit(int32_t r, RuneSet* out) {
   out->add(r, r);
-  return true;
+  for (int32_t x = fold_next(r); x >= 0 && x != r; x = fold_next(x)) out->add(x, x);
 }
 
 struct Group {
@@ -176,7 +177,7 @@ class GoParser {
   ReP literal(int32_t c) {
     RuneSet s;
     if (flags_ & kFoldCase) {
-      if (!fold_orbit(c, &s)) { unsupported("(?i) applied to a non-ASCII cased rune"); s.add(c, c); }
+      fold_orbit(c, &s);
     } else {
       s.add(c, c);
     }
@@ -188,9 +189,7 @@ class GoParser {
     if ((lo <= kMinFold && hi >= kMaxFold) || hi < kMinFold || lo > kMaxFold) { s->add(lo, hi); return; }
     if (lo < kMinFold) { s->add(lo, kMinFold - 1); lo = kMinFold; }
     if (hi > kMaxFold) { s->add(kMaxFold + 1, hi); hi = kMaxFold; }
-    for (int32_t x = lo; x <= hi; ++x) {
-      if (!fold_orbit(x, s)) { unsupported("(?i) range over non-ASCII cased runes"); s->add(x, x); }
-    }
+    for (int32_t x = lo; x <= hi; ++x) fold_orbit(x, s);
   }
 
   void add_range(RuneSet* s, int32_t lo, int32_t hi) {
@@ -294,7 +293,15 @@ class GoParser {
       unsupported("unicode script classes");
       tab.add(0, kMaxRune);
     }
-    if ((flags_ & kFoldCase) && folds) unsupported("(?i) with a case-folding unicode category");
+    if ((flags_ & kFoldCase) && folds) {
+      // [Go stdlib] unicode.FoldCategory: the runes outside the category that
+      // simple-fold to runes inside it -- the category's orbit closure
+      RuneSet closed;
+      tab.normalize();
+      for (const auto& rg : tab.ranges())
+        for (int32_t x = std::max(rg.first, kMinFold); x <= std::min(rg.second, kMaxFold); ++x) fold_orbit(x, &closed);
+      tab.add(closed);
+    }
     tab.normalize();
     if (sign < 0) tab.negate();
     s->add(tab);

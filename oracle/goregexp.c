@@ -104,26 +104,25 @@ static int cls_has(const int* r, int n, int x) {
 }
 
 /* ---- case folding --------------------------------------------------------
- * [Go stdlib] unicode.SimpleFold orbits. Only the orbits reachable from ASCII
- * letters are modelled: {X,x} for every letter, plus {K,k,U+212A} and
- * {S,s,U+017F}. Any other cased rune under (?i) sets `unsupported`. */
-static int cased_nonascii(int r) {
-  return r >= 0x80 && cls_has((const int*)orc_cased, orc_ncased * 2, r);
-}
-/* returns orbit size (members written to out[]), or -1 if unknown */
-static int fold_orbit(int r, int out[3]) {
-  if ((r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z')) {
-    int l = r | 0x20, u = r & ~0x20;
-    out[0] = u; out[1] = l;
-    if (l == 'k') { out[2] = 0x212A; return 3; }
-    if (l == 's') { out[2] = 0x17F; return 3; }
-    return 2;
+ * [Go stdlib] unicode.SimpleFold: orc_fold lists, sorted by rune, the next
+ * member of every simple-case-folding orbit of two or more runes (generated
+ * from Unicode 13.0, the version of Go 1.18's tables; at most 4 members). */
+static int fold_next(int r) {
+  int lo = 0, hi = orc_nfold;
+  while (lo < hi) {
+    int m = (lo + hi) / 2, x = (int)orc_fold[2 * m];
+    if (x == r) return (int)orc_fold[2 * m + 1];
+    if (x < r) lo = m + 1;
+    else hi = m;
   }
-  if (r == 0x212A) { out[0] = 'K'; out[1] = 'k'; out[2] = 0x212A; return 3; }
-  if (r == 0x17F) { out[0] = 'S'; out[1] = 's'; out[2] = 0x17F; return 3; }
-  if (cased_nonascii(r)) return -1;
-  out[0] = r;
-  return 1;
+  return -1;
+}
+/* the orbit of r, r first; returns its size (1..4) */
+static int fold_orbit(int r, int out[4]) {
+  int k = 0;
+  out[k++] = r;
+  for (int x = fold_next(r); x >= 0 && x != r && k < 4; x = fold_next(x)) out[k++] = x;
+  return k;
 }
 
 /* ---- AST (regexp/syntax.Regexp) ------------------------------------------- */
@@ -199,10 +198,6 @@ static int next_rune(Parser* p, const unsigned char** t, const unsigned char* en
 /* p.literal(r) */
 static void p_literal(Parser* p, int r) {
   Node* n = node_new(OP_LITERAL, p->flags);
-  if (p->flags & F_FOLD) {
-    int o[3];
-    if (fold_orbit(r, o) < 0) unsup(p, "(?i) on a non-ASCII cased rune");
-  }
   cls_push(&n->cls, r, r);
   p_push(p, n);
 }
@@ -216,10 +211,8 @@ static void append_folded_range(Parser* p, Class* c, int lo, int hi) {
   if (lo < MIN_FOLD) { cls_push(c, lo, MIN_FOLD - 1); lo = MIN_FOLD; }
   if (hi > MAX_FOLD) { cls_push(c, MAX_FOLD + 1, hi); hi = MAX_FOLD; }
   for (int x = lo; x <= hi; x++) {
-    int o[3];
+    int o[4];
     int k = fold_orbit(x, o);
-    if (k < 0) { unsup(p, "(?i) range over non-ASCII cased runes"); cls_push(c, x, x); continue; }
-    cls_push(c, x, x);
     for (int i = 0; i < k; i++) cls_push(c, o[i], o[i]);
   }
 }
@@ -353,7 +346,21 @@ static int parse_unicode_class(Parser* p, const unsigned char** t, const unsigne
     }
   }
   if (!found) { free(tmp.r); fail(p, "invalid character class range (unicode name)"); return -1; }
-  if ((p->flags & F_FOLD) && fold_tab) unsup(p, "(?i) with a folding unicode category");
+  if ((p->flags & F_FOLD) && fold_tab) {
+    /* FoldCategory (parseUnicodeClass): add the runes that simple-fold into the table */
+    Class closed = {0};
+    cls_clean(&tmp);
+    for (int i = 0; i < tmp.n; i += 2) {
+      int lo = tmp.r[i] < MIN_FOLD ? MIN_FOLD : tmp.r[i], hi = tmp.r[i + 1] > MAX_FOLD ? MAX_FOLD : tmp.r[i + 1];
+      for (int x = lo; x <= hi; x++) {
+        int o[4];
+        int k = fold_orbit(x, o);
+        for (int j = 1; j < k; j++) cls_push(&closed, o[j], o[j]);
+      }
+    }
+    for (int i = 0; i < closed.n; i += 2) cls_push(&tmp, closed.r[i], closed.r[i + 1]);
+    free(closed.r);
+  }
   cls_clean(&tmp);
   if (sign < 0) cls_negate(&tmp);
   for (int i = 0; i < tmp.n; i += 2) cls_push(c, tmp.r[i], tmp.r[i + 1]);
@@ -973,9 +980,8 @@ static int rune_match(const Inst* in, int r) {
     case I_ANYNOTNL: return r != '\n';
     case I_RUNE: return cls_has(in->r, in->nr, r);
     case I_RUNEFOLD: {
-      int o[3];
+      int o[4];
       int k = fold_orbit(in->r[0], o);
-      if (r == in->r[0]) return 1;
       for (int i = 0; i < k; i++) if (o[i] == r) return 1;
       return 0;
     }

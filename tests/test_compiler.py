@@ -125,3 +125,67 @@ def test_keyword_alternation_compiles():
     want = O.grep_map(pat, data)
     for g, w in zip(got, want):
         np.testing.assert_array_equal(g, w)
+
+
+FOLD_ATOMS = ["(?i)é", "(?i)σ", "(?i)ς", "(?i)ß", "(?i)ẞ", "(?i)µ", "(?i)θ", "(?i)i", "(?i)İ", "(?i)ı", "(?i)д",
+              "(?i)[α-ω]", "(?i)[^é]", "(?i)\\pL", "(?i)\\p{Lu}", "(?i)\\P{Ll}", "(?i)\\p{Mn}", "(?i)[\\x{100}-\\x{17f}]",
+              "(?i)Å", "(?i)k", "(?i)[ǅ]", "é", "σ", "\\pL", "."]
+FOLD_ALPHA = [s.encode() for s in ["é", "É", "e", "σ", "ς", "Σ", "ß", "ẞ", "ss", "µ", "μ", "Μ", "θ", "ϑ", "ϴ", "Θ", "i", "I",
+                                   "İ", "ı", "д", "Д", "Å", "å", "Å", "k", "K", "K", "ǅ", "Ǆ", "ǆ", "ͅ", "ι", "ι", "ā", "Ā",
+                                   "ſ", "x", " ", "1", "\n"]] + [b"\xff", b"\xce"]
+
+
+def test_compiler_vs_oracle_unicode_folding():
+    """(?i) over non-ASCII runes and folding categories (unicode.SimpleFold
+    orbits, unicode.FoldCategory): the product's DFA and the oracle's Pike VM,
+    both built from the generated Unicode 13.0 orbit table, agree on random
+    patterns and lines (parity of the orbit table itself is unpinned)."""
+    rnd = random.Random(7)
+    checked = 0
+    for it in range(250):
+        pat = "".join(rnd.choice(FOLD_ATOMS) for _ in range(rnd.randint(1, 3)))
+        if rnd.random() < 0.3:
+            pat = "(%s)|%s" % (pat, rnd.choice(FOLD_ATOMS))
+        pat = pat.encode()
+        assert O.compile_status(pat) == O.ORC_OK, pat
+        cp = _compile(pat)
+        assert cp != "UNSUP", pat
+        for _ in range(16):
+            data = b"".join(rnd.choice(FOLD_ALPHA) for _ in range(rnd.randint(0, 10)))
+            got = run_blob(cp, data)
+            want = O.grep_map(pat, data)
+            for g, w in zip(got, want):
+                np.testing.assert_array_equal(g, w, err_msg=repr((pat, data)))
+            checked += 1
+    assert checked == 4000
+
+
+def test_fold_orbit_table_shape():
+    """The generated orbit table (tools/gen_unicode_tables.py): cyclic, closed,
+    at most 4 runes per orbit, and the orbits Go documents."""
+    import re as _re
+
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "distributed-grep_amd", "csrc", "compiler", "unicode_tables.inc")).read()
+    m = _re.search(r"dg_fold\[\] = \{([^}]*)\}", src)
+    vals = [int(x, 16) for x in m.group(1).split(",")]
+    nxt = dict(zip(vals[0::2], vals[1::2]))
+
+    def orbit(r):
+        out, x = {r}, nxt.get(r)
+        while x is not None and x != r:
+            out.add(x)
+            x = nxt[x]
+        return out
+
+    for r in nxt:
+        assert nxt[r] in nxt and r in orbit(nxt[r]) and len(orbit(r)) <= 4
+    assert orbit(ord("k")) == {ord("k"), ord("K"), 0x212A}
+    assert orbit(ord("s")) == {ord("s"), ord("S"), 0x17F}
+    assert orbit(0x3C3) == {0x3A3, 0x3C3, 0x3C2}
+    assert orbit(0xDF) == {0xDF, 0x1E9E}
+    assert orbit(0x3B8) == {0x398, 0x3B8, 0x3D1, 0x3F4}
+    assert orbit(0x345) == {0x345, 0x399, 0x3B9, 0x1FBE}
+    assert 0x130 not in nxt and 0x131 not in nxt and orbit(ord("i")) == {ord("i"), ord("I")}

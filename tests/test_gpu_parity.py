@@ -535,7 +535,7 @@ def test_forced_steppers_agree_on_c3(gpu_ctx, mode):
         gpu_ctx.set_stepper("auto")
 
 
-@pytest.mark.parametrize("pattern", [b"a[ab]{15}$", b"a[ab]{16}$", b"(?i)b[ab]{14}[^b]$"])
+@pytest.mark.parametrize("pattern", [b"a[ab]{15}$", b"a[ab]{16}$", b"(?i)b[ab]{15}[^b]$"])
 def test_dfa_beyond_65535_states(gpu_ctx, pattern):
     """DFAs of 65,536 .. 2^21 states (the compiler's budget): the filter keeps
     the shallowest rows in LDS and verifies candidate lines on the whole DFA,
@@ -552,3 +552,17 @@ def test_dfa_beyond_65535_states(gpu_ctx, pattern):
     assert n > 0
     st = gpu_ctx.scan_stats()
     assert st["stepper"] == "filter" and st["candidates"] > 0, st
+
+
+@pytest.mark.parametrize("pattern", ["(?i)é", "(?i)σ+", "(?i)straße", "(?i)\\p{Lu}x", "(?i)[α-ω]{2}", "(?i)\\P{Ll}k",
+                                     "(?i)(kelvin|ſ|µ)"])
+def test_unicode_case_folding(gpu_ctx, pattern):
+    """(?i) over non-ASCII runes: unicode.SimpleFold orbits and FoldCategory
+    (generated from Unicode 13.0; parity of the table is unpinned)."""
+    rnd = random.Random(pattern)
+    alpha = [s.encode() for s in ["é", "É", "e", "σ", "ς", "Σ", "ß", "ẞ", "ss", "STRASSE", "straße", "STRAẞE", "µ",
+                                  "Μ", "K", "kelvin", "ſ", "α", "Ω", "x", "X", " ", "\n", "\n"]] + [b"\xff"]
+    data = b"".join(rnd.choice(alpha) for _ in range(60000))
+    pattern = pattern.encode()
+    n = _check(gpu_ctx, pattern, data, threads=16)
+    assert n > 0
