@@ -77,7 +77,9 @@ def parse():
                     help="CPU baseline budget: whole 1 MiB pieces of the split until this much time is spent")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-windows", type=int, default=6)
-    ap.add_argument("--lane-chunk", type=int, default=0, help="tuning: force the Sheng lane chunk (0 = adaptive)")
+    ap.add_argument("--lane-chunk", type=int, default=0, help="tuning: force the Sheng/pair/filter lane chunk (0 = adaptive)")
+    ap.add_argument("--pattern", default=None,
+                    help="ablation only: scan the workload's split with this pattern instead (not a BASELINE config)")
     return ap.parse_args()
 
 
@@ -103,7 +105,7 @@ def main():
     gib = args.split_gib if args.split_gib is not None else wl["gib"]
     n = int(gib * (1 << 30))
     n -= n % 64
-    pattern = workload_pattern(wl)
+    pattern = args.pattern if args.pattern is not None else workload_pattern(wl)
 
     ctx = dgrep.Context(local)
     if args.lane_chunk:
@@ -205,7 +207,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded log corpus generated in HBM, SURVEY.md §8d)",
             "config": {
-                "workload": wl["desc"] if world == 1 else wl["desc"] + "; one split per GPU + RCCL gather of match records to rank 0",
+                "workload": (wl["desc"] if world == 1 else wl["desc"] + "; one split per GPU + RCCL gather of match records to rank 0")
+                            + ("" if args.pattern is None else "; ABLATION: pattern overridden"),
                 "pattern": pattern if len(pattern) < 200 else pattern[:120] + "...(%d bytes)" % len(pattern),
                 "split_bytes_per_gpu": n,
                 "total_bytes": n * world,
@@ -234,9 +237,12 @@ def main():
                 "kernel_ms_median": round(kern_med, 4),
                 "kernel_ms_min": round(float(np.min(kms)), 4),
                 "overflow_ms_avg": round(float(np.mean([x["overflow_ms"] for x in stats])), 4),
+                "verify_ms_avg": round(float(np.mean([x["verify_ms"] for x in stats])), 4),
+                "scan_ms_avg": round(float(np.mean([x["scan_ms"] for x in stats])), 4),
+                "candidates_dropped": int(st["candidates"]),
                 "overflow_lanes": int(st["overflow_lanes"]),
-                "timing": "HIP events on the launch stream around the scan kernel and the overflow pass "
-                          "(dgrep_last_kernel_ms), averaged over the timed steps",
+                "timing": "HIP events on the launch stream around the scan kernel, the overflow pass and (filter "
+                          "stepper) the candidate verification (dgrep_last_kernel_ms), averaged over the timed steps",
                 "algorithmic_bytes_per_launch": int(n + STAGED_LINE_BYTES * count),
             },
             "cpu_baseline": cpu,
