@@ -58,6 +58,10 @@ struct ScanArgs {
   // kStepFilter only: the premultiplied CAND_END state (a '\n' ends a line that
   // left the LDS-resident part of the DFA: a candidate, verified afterwards)
   uint32_t cand_end;
+  // one-chunk-per-lane steppers: per resident thread, spill_per_lane records of
+  // HBM the lane moves its full LDS slots to (nullptr: no spilling)
+  uint2* spill;
+  uint32_t spill_per_lane;
 };
 
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids

@@ -471,6 +471,8 @@ struct Emitter {
   uint64_t cs;
   uint64_t out_base;     // first staging index of this lane (direct mode)
   uint32_t nl_prefix;    // '\n' between tile start and chunk start (direct mode)
+  uint2* spill = nullptr;    // slot mode: this lane's HBM spill area (nullptr: none)
+  uint32_t spill_cap = 0;    // its records
 
   // cand: a filter candidate (kCandidateBit in len, verified afterwards)
   __device__ __forceinline__ void operator()(LaneRun& r, uint64_t q, int64_t start, uint32_t rel,
@@ -486,10 +488,18 @@ struct Emitter {
         L.rel = nl_prefix + rel;
         a->staging[o] = L;
       }
-    } else if (r.nev < uint32_t(E)) {
-      // start <= C and rel <= C fit 16 bits each
-      slots[r.nev * 2 + 0] = uint32_t(start) | (rel << 16);
-      slots[r.nev * 2 + 1] = lw;
+    } else {
+      // start < C and rel < C fit 16 bits each
+      const uint32_t w0 = uint32_t(start) | (rel << 16);
+      if (r.nev < uint32_t(E)) {
+        slots[r.nev * 2 + 0] = w0;
+        slots[r.nev * 2 + 1] = lw;
+      } else if (r.nev - uint32_t(E) < spill_cap) {
+        // LDS slots full: the lane's further records go to its spill area in
+        // HBM (read back at the tile's end), so a dense pattern neither caps
+        // the lane chunk nor sends the lane to the overflow pass
+        spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
+      }
     }
     if (len > 0xffffffffull) atomicOr(a->status, kStatusLineTooLong);
     if (cand && len >= uint64_t(kCandidateBit)) atomicOr(a->status, kStatusCandidateTooLong);
@@ -992,7 +1002,11 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         nlc[1] = run_lane<BK>(a, st, cs[1], r[1], e1, C);
       }
     } else {
-      const Emitter<E, false> em{&a, slots, cs[0], 0, 0};
+      Emitter<E, false> em{&a, slots, cs[0], 0, 0};
+      if (a.spill) {
+        em.spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane;
+        em.spill_cap = a.spill_per_lane;
+      }
       if constexpr (kStaged) {
         if (full)
           nlc[0] = run_lane_staged<Tune<Step>::C, R>(a, st, cs[0], lane, stage + (tid >> 6) * (DGREP_STAGE_DEPTH * 64 * R), r[0],
@@ -1031,15 +1045,25 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
     for (int k = 0; k < S; ++k) {
       const uint32_t nev = r[k].nev;
       const uint32_t* sl = slots + k * E * 2;
+      const bool spill = S == 1 && a.spill;
+      const uint2* sp = spill ? a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane : nullptr;
       const uint64_t o0 = base + ev_off[k];
-      if (nev <= uint32_t(E)) {
+      if (nev <= uint32_t(E) + (spill ? a.spill_per_lane : 0u)) {
         for (uint32_t j = 0; j < nev; ++j) {
           const uint64_t o = o0 + j;
           if (o < a.capacity) {
-            const uint32_t w0 = sl[j * 2 + 0];
+            uint32_t w0, w1;
+            if (j < uint32_t(E)) {
+              w0 = sl[j * 2 + 0];
+              w1 = sl[j * 2 + 1];
+            } else {
+              const uint2 w = sp[j - uint32_t(E)];
+              w0 = w.x;
+              w1 = w.y;
+            }
             StagedLine L;
             L.start = cs[k] + (w0 & 0xffffu);
-            L.len = sl[j * 2 + 1];
+            L.len = w1;
             L.rel = nl_off[k] + (w0 >> 16);
             a.staging[o] = L;
           }
@@ -1352,13 +1376,18 @@ struct TileOp {
   uint32_t force;
   double density;  // matching lines per byte seen by the previous scan (0: unknown)
   uint32_t* slots;
+  uint32_t spill_per_lane;
   template <class S, int T>
   hipError_t run() const {
     uint64_t c = uint64_t(Tune<S>::C);
-    *slots = uint32_t(Tune<S>::E);
-    // at most a quarter of the slots expected in use: an overflowing lane costs
-    // two latency-bound passes of the overflow kernel over its chunk
-    const uint64_t dens_cap = density > 0 ? uint64_t(double(Tune<S>::E) / (4.0 * density)) : 0;
+    // a lane's record capacity: its LDS slots, plus the HBM spill area of the
+    // one-chunk-per-lane steppers
+    constexpr uint32_t E = uint32_t(Tune<S>::E);
+    const uint32_t cap = E + (adaptive_chunk<S, T>() ? spill_per_lane : 0u);
+    *slots = cap;
+    // at most a quarter of the capacity expected in use: an overflowing lane
+    // costs two latency-bound passes of the overflow kernel over its chunk
+    const uint64_t dens_cap = density > 0 ? uint64_t(double(cap) / (4.0 * density)) : 0;
     if constexpr (adaptive_chunk<S, T>())
       c = force ? uint64_t(force)
                 : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap);
@@ -1390,9 +1419,13 @@ struct OverflowOp {
 }  // namespace
 
 uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t resident_blocks, uint32_t force,
-                         double density, uint32_t* chunk, uint32_t* waves_per_block, uint32_t* slots) {
+                         double density, uint32_t spill_per_lane, uint32_t* chunk, uint32_t* waves_per_block,
+                         uint32_t* slots, uint32_t* threads, bool* spills) {
   uint64_t b = 0;
-  (void)dispatch(kind, table_bytes, TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots});
+  (void)dispatch(kind, table_bytes,
+                 TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots, spill_per_lane});
+  *threads = *waves_per_block * 64;
+  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepFilter;
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {

@@ -32,11 +32,17 @@
 #ifndef DGREP_PAIR_ENABLE
 #define DGREP_PAIR_ENABLE 1
 #endif
+// matching-line records per resident thread of the HBM spill area the
+// one-chunk-per-lane steppers move full LDS slots to (0: no spilling)
+#ifndef DGREP_SPILL_RECORDS
+#define DGREP_SPILL_RECORDS 240
+#endif
 
 namespace dgrep {
 // scan_dfa.hip
 uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t resident_blocks, uint32_t force,
-                         double density, uint32_t* chunk, uint32_t* waves_per_block, uint32_t* slots);
+                         double density, uint32_t spill_per_lane, uint32_t* chunk, uint32_t* waves_per_block,
+                         uint32_t* slots, uint32_t* threads, bool* spills);
 uint32_t scan_table_row();
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu);
 hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
@@ -99,6 +105,8 @@ struct dgrep_ctx {
   unsigned long long* d_counters = nullptr;
   OverflowLane* d_overflow = nullptr;
   uint64_t overflow_cap = 0;
+  uint2* d_spill = nullptr;  // HBM spill areas of the resident threads (ScanArgs::spill)
+  uint64_t spill_cap = 0;
 
   // dgrep_scan (host data) buffers
   uint8_t* d_data = nullptr;
@@ -330,7 +338,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_cls, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_cls, c->d_spill, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -572,9 +580,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     return DGREP_E_INVALID;
   }
   const uint64_t resident = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
-  uint32_t chunk = 0, wpb = 1, slots = 0;
-  const uint64_t tile = scan_tile_bytes(c->step_kind, c->table_bytes, n, resident, c->lane_chunk, c->density, &chunk,
-                                        &wpb, &slots);
+  uint32_t chunk = 0, wpb = 1, slots = 0, threads = 0;
+  bool spills = false;
+  const uint64_t tile = scan_tile_bytes(c->step_kind, c->table_bytes, n, resident, c->lane_chunk, c->density,
+                                        DGREP_SPILL_RECORDS, &chunk, &wpb, &slots, &threads, &spills);
   const uint64_t ntiles = (n + tile - 1) / tile;
   int rc;
   if ((rc = grow(c, &c->d_tiles, &c->tiles_cap, ntiles)) != DGREP_OK) return rc;
@@ -588,6 +597,11 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     return rc;
 
   if (!c->d_overflow && (rc = grow(c, &c->d_overflow, &c->overflow_cap, 1u << 16)) != DGREP_OK) return rc;
+  const int grid = int(std::min<uint64_t>(ntiles, resident));
+  const bool use_spill = spills && DGREP_SPILL_RECORDS > 0;
+  if (use_spill &&
+      (rc = grow(c, &c->d_spill, &c->spill_cap, uint64_t(grid) * threads * DGREP_SPILL_RECORDS)) != DGREP_OK)
+    return rc;
 
   ScanArgs a;
   memset(&a, 0, sizeof a);
@@ -610,12 +624,13 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.pair_thr = c->pair_args.thr;
   a.pair_div = c->pair_args.div;
   a.cand_end = c->cand_end;
+  a.spill = use_spill ? c->d_spill : nullptr;
+  a.spill_per_lane = use_spill ? DGREP_SPILL_RECORDS : 0;
   // every resident workgroup is launched even when the last round of tiles is
   // part-empty: trimming the grid so that every wave runs the same number of
   // tiles leaves some CUs with 2 workgroups and others with 3, and the time
   // follows the fullest CU (C2 16 KiB chunks: 4.13 TB/s trimmed, 4.74 full)
   (void)wpb;
-  const int grid = int(std::min<uint64_t>(ntiles, resident));
   unsigned long long ctr[4] = {0, 0, 0, 0};
   S.lane_chunk = chunk;
   S.lane_slots = slots;

@@ -203,15 +203,18 @@ def test_overflow_pass_dense_every_chunk(gpu_ctx, chunk):
     including lines that cross sub-chunk and chunk edges."""
     try:
         gpu_ctx.set_lane_chunk(chunk)
-        for maxlen in (4, 40, 700):
-            data = _dense_lines(chunk + maxlen, 40000 if maxlen < 100 else 8000, maxlen)
-            for pattern in (b"error", b"", b"b x"):
+        for maxlen in (4, 40, 700, 0):
+            # maxlen 0: 2-byte lines, more matching lines per lane than its LDS
+            # slots plus its HBM spill area hold -> the overflow pass
+            data = (_dense_lines(chunk + maxlen, 40000 if maxlen < 100 else 8000, maxlen) if maxlen else
+                    b"e\n" * 300000)
+            for pattern in (b"error", b"", b"b x", b"e"):
                 cp = gpu_ctx.load(pattern)
                 assert cp.nstates <= 8
-                _check(gpu_ctx, cp, data)
+                n = _check(gpu_ctx, cp, data)
                 st = gpu_ctx.scan_stats()
                 assert st["stepper"] == "sheng" and st["lane_chunk"] == chunk
-                if maxlen < 100:
+                if maxlen == 0 and n:
                     assert st["overflow_lanes"] > 0, st
     finally:
         gpu_ctx.set_lane_chunk(0)
