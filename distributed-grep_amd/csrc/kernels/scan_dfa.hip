@@ -505,6 +505,30 @@ struct Emitter {
     if (cand && len >= uint64_t(kCandidateBit)) atomicOr(a->status, kStatusCandidateTooLong);
     ++r.nev;
   }
+  // The same for a line wholly inside the lane's chunk (start < q < C <= 32 KiB):
+  // 32-bit chunk-relative positions, no length checks.
+  __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
+    const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
+    if (DIRECT) {
+      const uint64_t o = out_base + r.nev;
+      if (o < a->capacity) {
+        StagedLine L;
+        L.start = cs + uint64_t(start);
+        L.len = lw;
+        L.rel = nl_prefix + rel;
+        a->staging[o] = L;
+      }
+    } else {
+      const uint32_t w0 = start | (rel << 16);
+      if (r.nev < uint32_t(E)) {
+        slots[r.nev * 2 + 0] = w0;
+        slots[r.nev * 2 + 1] = lw;
+      } else if (r.nev - uint32_t(E) < spill_cap) {
+        spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
+      }
+    }
+    ++r.nev;
+  }
 };
 
 // Block-local bookkeeping shared by the 16 word steps of one 64-byte block.
@@ -571,7 +595,19 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
   else
     any = bool(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)));
   if (__builtin_expect(any, 0)) {
-    // a '\n' in this word ends a matching line: resolve it exactly
+    // a '\n' in this word ends a matching line. Common case (a single '\n' in
+    // the word, inside the chunk): that byte is the event, the line started
+    // after the previous '\n' (an earlier word of the block, or r.prev_nl), all
+    // positions are chunk-relative 32-bit values. Anything else (several '\n'
+    // in one word, the part past the chunk end) takes the general loop.
+    if (!b.past && (m & (m - 1u)) == 0u) {
+      // branch-free operands (selects, no nested exec-mask regions)
+      const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
+      const uint32_t lastpos = uint32_t(b.pos) + 4u * uint32_t(b.lastj) + hi_byte(b.lastm | 1u);
+      const uint32_t prev = b.lastm ? lastpos : uint32_t(r.prev_nl);
+      const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+      if (r.seen | (b.lastm != 0)) emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk));
+    } else {
     const uint64_t q0 = b.pos + 4u * J;
     const bool seen_w = r.seen || b.lastm != 0;
     const bool term_w = r.term || (b.past && b.lastm != 0);
@@ -592,6 +628,7 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
       const int64_t start = below ? int64_t(q0 + hi_byte(below)) + 1 : prev_w + 1;
       const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
       emit(r, q0 + k, start, b.nl0 + b.nlrun + uint32_t(__popc(below)), cand_of(st, sk));
+    }
     }
   }
   if constexpr (TRACK) {
