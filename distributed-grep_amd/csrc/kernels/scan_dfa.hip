@@ -133,7 +133,7 @@
 #ifndef DGREP_PAIR_WAVES
 #define DGREP_PAIR_WAVES 3
 #endif
-// Filter (C4, > 256 states): 1024-thread workgroups sharing one LDS image
+// Filter (C4, > 256 states): one 768-thread workgroup per CU shares one LDS image
 #ifndef DGREP_FILTER_CHUNK
 #define DGREP_FILTER_CHUNK 4096
 #endif
@@ -141,7 +141,7 @@
 #define DGREP_FILTER_SLOTS 4
 #endif
 #ifndef DGREP_FILTER_BLOCK
-#define DGREP_FILTER_BLOCK 64
+#define DGREP_FILTER_BLOCK 128
 #endif
 #ifndef DGREP_SHENG_SCHED_BARRIER
 #define DGREP_SHENG_SCHED_BARRIER 0
@@ -581,56 +581,75 @@ __device__ __forceinline__ void word_step2(const Step& st, uint32_t M, uint32_t 
   sb = b3;
 }
 
+// Does a word whose four DFA steps end in s0..s3 hold an event (a '\n' that
+// ends a matching line)?
+template <class Step>
+__device__ __forceinline__ bool word_any(const Step& st, uint32_t M, uint32_t s0, uint32_t s1, uint32_t s2,
+                                         uint32_t s3) {
+  if constexpr (Step::kKind == kStepSheng8)
+    return StepSheng8::any4(s0, s1, s2, s3, M);
+  else if constexpr (Step::kKind == kStepPair)
+    return st.any2(s1, s3);
+  else if constexpr (Step::kKind == kStepFilter)
+    return max(max(s0, s1), max(s2, s3)) >= M;
+  else
+    return bool(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)));
+}
+
+// The events of word J (newline mask m, states s0..s3), with `b` holding the
+// block's bookkeeping of the words before J. Common case (a single '\n' in
+// the word, inside the chunk): that byte is the event, the line started after
+// the previous '\n' (an earlier word of the block, or r.prev_nl), all positions
+// are chunk-relative 32-bit values. Anything else (several '\n' in one word,
+// the part past the chunk end) takes the general loop.
+template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
+                                          uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
+                                          const Emitter<E, DIRECT>& emit) {
+  if (!b.past && (m & (m - 1u)) == 0u) {
+    // branch-free operands (selects, no nested exec-mask regions)
+    const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
+    const uint32_t lastpos = uint32_t(b.pos) + 4u * uint32_t(b.lastj) + hi_byte(b.lastm | 1u);
+    const uint32_t prev = b.lastm ? lastpos : uint32_t(r.prev_nl);
+    const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+    if (r.seen | (b.lastm != 0)) emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk));
+    return;
+  }
+  const uint64_t q0 = b.pos + 4u * J;
+  const bool seen_w = r.seen || b.lastm != 0;
+  const bool term_w = r.term || (b.past && b.lastm != 0);
+  const int64_t prev_w = b.lastm ? int64_t(b.pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm)) : r.prev_nl;
+  uint32_t evm;
+  if constexpr (Step::kKind == kStepPair)
+    evm = st.evm(s1, s3);
+  else
+    evm = uint32_t(Step::is(s0, M)) | (uint32_t(Step::is(s1, M)) << 1) | (uint32_t(Step::is(s2, M)) << 2) |
+          (uint32_t(Step::is(s3, M)) << 3);
+  while (evm) {
+    const uint32_t k = uint32_t(__builtin_ctz(evm));
+    evm &= evm - 1;
+    const uint32_t below = m & ((1u << (8 * k)) - 1u);
+    bool ok = seen_w || below != 0;
+    if (b.past) ok = ok && !term_w && below == 0;  // only the first '\n' past the chunk end
+    if (!ok) continue;
+    const int64_t start = below ? int64_t(q0 + hi_byte(below)) + 1 : prev_w + 1;
+    const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+    emit(r, q0 + k, start, b.nl0 + b.nlrun + uint32_t(__popc(below)), cand_of(st, sk));
+  }
+}
+
+// newline bookkeeping of word J
+template <int J>
+__device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
+  b.nlrun += uint32_t(__popc(m));
+  if (m) { b.lastm = m; b.lastj = J; }
+}
+
 template <int J, bool TRACK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
                                             uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
-  bool any;
-  if constexpr (Step::kKind == kStepSheng8)
-    any = StepSheng8::any4(s0, s1, s2, s3, M);
-  else if constexpr (Step::kKind == kStepPair)
-    any = st.any2(s1, s3);
-  else if constexpr (Step::kKind == kStepFilter)
-    any = max(max(s0, s1), max(s2, s3)) >= M;
-  else
-    any = bool(int(Step::is(s0, M)) | int(Step::is(s1, M)) | int(Step::is(s2, M)) | int(Step::is(s3, M)));
-  if (__builtin_expect(any, 0)) {
-    // a '\n' in this word ends a matching line. Common case (a single '\n' in
-    // the word, inside the chunk): that byte is the event, the line started
-    // after the previous '\n' (an earlier word of the block, or r.prev_nl), all
-    // positions are chunk-relative 32-bit values. Anything else (several '\n'
-    // in one word, the part past the chunk end) takes the general loop.
-    if (!b.past && (m & (m - 1u)) == 0u) {
-      // branch-free operands (selects, no nested exec-mask regions)
-      const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
-      const uint32_t lastpos = uint32_t(b.pos) + 4u * uint32_t(b.lastj) + hi_byte(b.lastm | 1u);
-      const uint32_t prev = b.lastm ? lastpos : uint32_t(r.prev_nl);
-      const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
-      if (r.seen | (b.lastm != 0)) emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk));
-    } else {
-    const uint64_t q0 = b.pos + 4u * J;
-    const bool seen_w = r.seen || b.lastm != 0;
-    const bool term_w = r.term || (b.past && b.lastm != 0);
-    const int64_t prev_w = b.lastm ? int64_t(b.pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm)) : r.prev_nl;
-    uint32_t evm;
-    if constexpr (Step::kKind == kStepPair)
-      evm = st.evm(s1, s3);
-    else
-      evm = uint32_t(Step::is(s0, M)) | (uint32_t(Step::is(s1, M)) << 1) | (uint32_t(Step::is(s2, M)) << 2) |
-            (uint32_t(Step::is(s3, M)) << 3);
-    while (evm) {
-      const uint32_t k = uint32_t(__builtin_ctz(evm));
-      evm &= evm - 1;
-      const uint32_t below = m & ((1u << (8 * k)) - 1u);
-      bool ok = seen_w || below != 0;
-      if (b.past) ok = ok && !term_w && below == 0;  // only the first '\n' past the chunk end
-      if (!ok) continue;
-      const int64_t start = below ? int64_t(q0 + hi_byte(below)) + 1 : prev_w + 1;
-      const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
-      emit(r, q0 + k, start, b.nl0 + b.nlrun + uint32_t(__popc(below)), cand_of(st, sk));
-    }
-    }
-  }
+  if (__builtin_expect(word_any(st, M, s0, s1, s2, s3), 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
   if constexpr (TRACK) {
     if (r.p1 < 0) {
       // the chunk's first line piece: compose its transition map (LaneRun::mlo)
@@ -639,8 +658,44 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
       if (m) r.p1 = int32_t(b.pos + 4u * J + lim);
     }
   }
-  b.nlrun += uint32_t(__popc(m));
-  if (m) { b.lastm = m; b.lastj = J; }
+  word_nl<J>(m, b);
+}
+
+// Four words J..J+3 (J % 4 == 0) of a block: their DFA steps (each word's
+// state-independent prep still issued one word ahead), then ONE wave-uniform
+// event test for the 16 bytes -- inside it the words are resolved in order,
+// each with the bookkeeping of the words before it -- then the newline
+// bookkeeping. The event branch is entered once per 16 bytes instead of once
+// per word that holds an event in any of the wave's 64 lanes.
+template <int J, int NW, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void quad_step(const Step& st, uint32_t M, const uint32_t (&w)[NW],
+                                          typename Step::Pre& pre, uint32_t& s, Blk& b, LaneRun& r,
+                                          const Emitter<E, DIRECT>& emit) {
+  uint32_t q[4][4], m[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const typename Step::Pre cur = pre;
+    if (J + i + 1 < NW) pre = st.prep(w[J + i + 1 < NW ? J + i + 1 : 0]);
+    m[i] = nl_mask(w[J + i]);
+    st.apply(cur, s, q[i][0], q[i][1], q[i][2], q[i][3]);
+    s = q[i][3];
+  }
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) any = any | word_any(st, M, q[i][0], q[i][1], q[i][2], q[i][3]);
+  if (__builtin_expect(any, 0)) {
+    Blk t = b;
+#define DG_QE(I)                                                                     \
+  if (word_any(st, M, q[I][0], q[I][1], q[I][2], q[I][3]))                           \
+    word_emit<J + (I)>(st, M, m[I], q[I][0], q[I][1], q[I][2], q[I][3], t, r, emit); \
+  word_nl<J + (I)>(m[I], t);
+    DG_QE(0) DG_QE(1) DG_QE(2) DG_QE(3)
+#undef DG_QE
+  }
+  word_nl<J>(m[0], b);
+  word_nl<J + 1>(m[1], b);
+  word_nl<J + 2>(m[2], b);
+  word_nl<J + 3>(m[3], b);
 }
 
 __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const LaneRun& r) {
@@ -703,6 +758,18 @@ __device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uin
   blk_finish(bb, sb, rb);
 }
 
+// Event tests per 16 bytes (quad_step) for the steppers whose steps run ahead
+// of their bookkeeping; the u8 table (sched barriers per word, VGPR-bound) and
+// the wide stepper keep one test per word, as does the staged Sheng path (TRACK).
+#ifndef DGREP_QUADS
+#define DGREP_QUADS 1
+#endif
+template <class Step, bool TRACK>
+constexpr bool use_quads() {
+  return DGREP_QUADS && !TRACK &&
+         Step::kKind == kStepPair;
+}
+
 template <int BK, bool TRACK = false, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
@@ -720,17 +787,24 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
     w[4 * i + 3] = v[i].w;
   }
   typename Step::Pre pre = st.prep(w[0]);
+  if constexpr (use_quads<Step, TRACK>()) {
+#define DG_Q(J) \
+  if ((J) < NW) quad_step<((J) < NW ? (J) : 0)>(st, M, w, pre, s, b, r, emit);
+    DG_Q(0) DG_Q(4) DG_Q(8) DG_Q(12) DG_Q(16) DG_Q(20) DG_Q(24) DG_Q(28)
+#undef DG_Q
+  } else {
 #define DG_W(J)                                                                         \
   if ((J) < NW) {                                                                       \
     const typename Step::Pre cur = pre;                                                 \
     if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : 0]);                     \
     word_step<J, TRACK>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit);              \
   }
-  DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
-  DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
-  DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
-  DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
+    DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
+    DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
+    DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
+    DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
 #undef DG_W
+  }
   blk_finish(b, s, r);
 }
 
@@ -994,7 +1068,8 @@ constexpr int waves_per_simd() {
   return Step::kKind == kStepSheng8  ? DGREP_SHENG_WAVES
          : Step::kKind == kStepTable ? DGREP_TABLE_WAVES
          : Step::kKind == kStepPair  ? DGREP_PAIR_WAVES
-                                     : kWideThreads / 256;  // wide, filter: one 1024-thread workgroup per CU
+                                     : Step::kKind == kStepFilter ? kFilterThreads / 256
+                                                                  : kWideThreads / 256;  // one workgroup per CU
 }
 
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
@@ -1347,7 +1422,7 @@ uint32_t scan_table_row() { return kRow; }
 namespace {
 template <class Step>
 constexpr int threads_of() {
-  return Step::kKind == kStepWide || Step::kKind == kStepFilter ? kWideThreads : kScanThreads;
+  return Step::kKind == kStepWide ? kWideThreads : Step::kKind == kStepFilter ? kFilterThreads : kScanThreads;
 }
 template <class Step, int TBL>
 hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
