@@ -6,7 +6,8 @@
 namespace dgrep {
 
 struct EncodeArgs {
-  const uint8_t* data;        // the HBM-resident split
+  const uint8_t* data;        // the HBM-resident split (16-byte aligned)
+  uint64_t n;                 // its bytes (aligned 16-B reads never pass them)
   const uint64_t* line_no;    // scan records, ascending line order
   const uint64_t* start;
   const uint32_t* len;

@@ -100,6 +100,77 @@ uint32_t key_prefix_hash(const uint8_t* filename, uint64_t fn) {
 
 namespace {
 constexpr int kEncThreads = 256;
+
+// bit 7 of byte k set iff byte k of x is zero (exact)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) { return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
+// bit 7 of byte k set iff byte k of x needs JSON escaping or is not ASCII:
+// < 0x20, >= 0x80, '"', '\\', '<', '>', '&'
+__device__ __forceinline__ uint32_t special_bytes(uint32_t x) {
+  return zero_bytes(x & 0xe0e0e0e0u) | (x & 0x80808080u) | zero_bytes(x ^ 0x22222222u) | zero_bytes(x ^ 0x5c5c5c5cu) |
+         zero_bytes(x ^ 0x3c3c3c3cu) | zero_bytes(x ^ 0x3e3e3e3eu) | zero_bytes(x ^ 0x26262626u);
+}
+// byte mask (bit 7 of each byte) of the bytes at absolute positions [lo, hi)
+// within the aligned word at position w
+__device__ __forceinline__ uint32_t range_mask(uint64_t w, uint64_t lo, uint64_t hi) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (w + uint64_t(k) >= lo && w + uint64_t(k) < hi) m |= 0x80u << (8 * k);
+  return m;
+}
+
+// true iff the value bytes [st, st + L) encode as themselves (plain printable
+// ASCII, nothing to escape): aligned 16-byte reads + SWAR tests, no per-byte
+// loads. The common case of text logs; otherwise json_body's byte loop.
+__device__ __forceinline__ bool plain_value(const uint8_t* data, uint64_t n, uint64_t st, uint64_t L) {
+  const uint64_t e = st + L;
+  for (uint64_t q = st & ~uint64_t(15); q < e; q += 16) {
+    if (q + 16 > n) {
+      for (uint64_t i = q > st ? q : st; i < e; ++i) {
+        const uint32_t b = data[i];
+        if (b < 0x20 || b >= 0x80 || b == '"' || b == '\\' || b == '<' || b == '>' || b == '&') return false;
+      }
+      return true;
+    }
+    const uint4 v = *reinterpret_cast<const uint4*>(data + q);
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    uint32_t bad = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t w = q + 4u * uint32_t(k);
+      const uint32_t in = (w >= st && w + 4 <= e) ? 0x80808080u : range_mask(w, st, e);
+      bad |= special_bytes(ws[k]) & in;
+    }
+    if (bad) return false;
+  }
+  return true;
+}
+
+// dst[0:L) = src[0:L) with 4-byte stores after the head: the source is read in
+// aligned dwords and realigned with v_alignbyte (whole-dword reads never pass
+// the source's last dword, which lies inside the 16-B-aligned split).
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t L) {
+  uint64_t i = 0;
+  while (i < L && (reinterpret_cast<uintptr_t>(dst + i) & 3)) {
+    dst[i] = src[i];
+    ++i;
+  }
+  if (L - i >= 8) {
+    const uint8_t* s = src + i;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(s) & 3);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(s - sh);
+    uint32_t* dw = reinterpret_cast<uint32_t*>(dst + i);
+    const uint64_t nd = (L - i) / 4 - 1;  // the last dword needs sw[k + 1], which may lie past the value: leave it
+    uint32_t lo = sw[0];
+    for (uint64_t k = 0; k < nd; ++k) {
+      const uint32_t hi = sw[k + 1];
+      dw[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh * 8u) : lo;
+      lo = hi;
+    }
+    i += nd * 4;
+  }
+  for (; i < L; ++i) dst[i] = src[i];
+}
 // {"Key":" + name + " (line number #" + digits + ")" + ,"Value":" + value + "}\n
 constexpr uint32_t kFixedBytes = 8 + 15 + 2 + 10 + 3;
 
@@ -126,7 +197,8 @@ __global__ __launch_bounds__(kEncThreads) void encode_measure_kernel(EncodeArgs 
     part[i] = uint16_t((h & 0x7fffffffu) % a.nreduce);
     idx[i] = uint32_t(i);
     const uint64_t st = a.start[i], L = a.len[i];
-    enc_len[i] = kFixedBytes + a.fname_json_len + nd + json_body<false>(a.data + st, L, nullptr);
+    const uint64_t body = plain_value(a.data, a.n, st, L) ? L : json_body<false>(a.data + st, L, nullptr);
+    enc_len[i] = kFixedBytes + a.fname_json_len + nd + body;
   }
 }
 
@@ -173,7 +245,14 @@ __global__ __launch_bounds__(kEncThreads) void encode_write_kernel(EncodeArgs a,
     }
     o += nd;
     put_str(o, ")\",\"Value\":\"");
-    o += json_body<true>(a.data + a.start[i], a.len[i], o);
+    const uint64_t L = a.len[i];
+    if (len_sorted[j] == kFixedBytes + a.fname_json_len + nd + L) {
+      // the measure pass found nothing to escape: the value is copied as is
+      copy_bytes(o, a.data + a.start[i], L);
+      o += L;
+    } else {
+      o += json_body<true>(a.data + a.start[i], L, o);
+    }
     put_str(o, "\"}\n");
   }
 }

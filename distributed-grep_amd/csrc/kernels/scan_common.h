@@ -127,14 +127,14 @@ constexpr uint32_t kWideHotBytes = DGREP_WIDE_HOT_KIB * 1024;
 #define DGREP_WIDE_THREADS 1024
 #endif
 constexpr int kWideThreads = DGREP_WIDE_THREADS;  // one workgroup per CU shares one LDS copy
-// The filter's one workgroup per CU: 768 threads = 3 waves per SIMD, which
-// leaves 168 VGPRs for 128-byte load blocks. (1024 threads with 64-byte blocks
-// fetched 1.82x the split from HBM: each lane's half-read 128-byte lines are
-// evicted before their second half is read -- tools/fetch_calib.hip measures
-// the same 1.8x for the bare 64-byte per-lane pattern at 768 lanes per CU and
-// 1.0x for 128-byte blocks.)
+// The filter's one workgroup per CU: 1024 threads (4 waves per SIMD) with
+// 128-byte load blocks. With 64-byte blocks it fetched 1.82x the split from
+// HBM (each lane's half-read 128-byte lines are evicted before their second
+// half is read; tools/fetch_calib.hip measures 1.8x for the bare 64-byte
+// per-lane pattern and 1.0x for 128-byte blocks). C4 kernel GB/s: 1024 / 128 B
+// 3,163; 1024 / 64 B 2,900; 768 / 128 B 2,743; 512 / 128 B 2,449.
 #ifndef DGREP_FILTER_THREADS
-#define DGREP_FILTER_THREADS 768
+#define DGREP_FILTER_THREADS 1024
 #endif
 constexpr int kFilterThreads = DGREP_FILTER_THREADS;
 

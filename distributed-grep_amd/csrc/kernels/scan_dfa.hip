@@ -133,7 +133,7 @@
 #ifndef DGREP_PAIR_WAVES
 #define DGREP_PAIR_WAVES 3
 #endif
-// Filter (C4, > 256 states): one 768-thread workgroup per CU shares one LDS image
+// Filter (C4, > 256 states): one 1024-thread workgroup per CU shares one LDS image
 #ifndef DGREP_FILTER_CHUNK
 #define DGREP_FILTER_CHUNK 4096
 #endif
@@ -761,8 +761,10 @@ __device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uin
 // Event tests per 16 bytes (quad_step) for the steppers whose steps run ahead
 // of their bookkeeping; the u8 table (sched barriers per word, VGPR-bound) and
 // the wide stepper keep one test per word, as does the staged Sheng path (TRACK).
+// (measured on C3 / Pair: 3,644 GB/s with quads vs 3,699 without -- the extra
+// live states cost more than the saved branches; off by default)
 #ifndef DGREP_QUADS
-#define DGREP_QUADS 1
+#define DGREP_QUADS 0
 #endif
 template <class Step, bool TRACK>
 constexpr bool use_quads() {
@@ -1288,8 +1290,12 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
           L.len &= ~kCandidateBit;
           const uint64_t a = L.start, e = L.start + L.len;
           uint32_t st = v.start;
+          // the next 16-byte piece is loaded while this one is stepped (the
+          // line's bytes come from HBM: the scan read them long ago)
+          uint4 nxt = *reinterpret_cast<const uint4*>(v.data + (a & ~uint64_t(15)));
           for (uint64_t q = a & ~uint64_t(15); q < e; q += 16) {
-            const uint4 w = *reinterpret_cast<const uint4*>(v.data + q);
+            const uint4 w = nxt;
+            if (q + 16 < e) nxt = *reinterpret_cast<const uint4*>(v.data + q + 16);
             const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
             for (int j = 0; j < 16; ++j) {

@@ -865,7 +865,7 @@ extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_res
 }
 
 // ---- partition + intermediate writer (map_reduce/worker.go:13-17,78-109) ----
-static int encode_resident(dgrep_ctx* c, const uint8_t* d_data, const uint64_t* d_line, const uint64_t* d_start,
+static int encode_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, const uint64_t* d_line, const uint64_t* d_start,
                            const uint32_t* d_len, uint64_t count, const char* filename, size_t fn, uint32_t nreduce,
                            uint8_t* d_out, uint64_t out_cap, uint64_t* begin, uint64_t* end, uint64_t* total) {
   if (nreduce == 0 || nreduce > 65535) { c->err = "nreduce must be 1..65535"; return DGREP_E_INVALID; }
@@ -881,6 +881,7 @@ static int encode_resident(dgrep_ctx* c, const uint8_t* d_data, const uint64_t* 
   if ((rc = grow(c, &c->d_bounds, &c->bounds_cap, 2 * uint64_t(nreduce) + 1)) != DGREP_OK) return rc;
   EncodeArgs a;
   a.data = d_data;
+  a.n = n;
   a.line_no = d_line;
   a.start = d_start;
   a.len = d_len;
@@ -916,7 +917,7 @@ extern "C" int dgrep_encode_device(dgrep_ctx* c, const void* d_data, size_t n, c
       (n && !d_data) || (out_cap && !d_out))
     return DGREP_E_INVALID;
   HIPCHK(hipSetDevice(c->device));
-  return encode_resident(c, static_cast<const uint8_t*>(d_data), d_line_no, d_start, d_len, count, filename, fn,
+  return encode_resident(c, static_cast<const uint8_t*>(d_data), n, d_line_no, d_start, d_len, count, filename, fn,
                          nreduce, static_cast<uint8_t*>(d_out), out_cap, part_begin, part_end, total);
 }
 
@@ -936,7 +937,8 @@ extern "C" int dgrep_map_partitions(dgrep_ctx* c, const uint8_t* data, size_t n,
   const uint8_t* dd = c->d_data ? c->d_data : reinterpret_cast<const uint8_t*>(c->d_counters);
   uint64_t total = 0;
   for (int attempt = 0; attempt < 2; ++attempt) {
-    if ((rc = encode_resident(c, dd, c->d_res_line, c->d_res_start, c->d_res_len, count, filename, fn, nreduce,
+    if ((rc = encode_resident(c, dd, c->d_data ? n : 0, c->d_res_line, c->d_res_start, c->d_res_len, count, filename,
+                              fn, nreduce,
                               c->d_enc_out, c->enc_out_cap, out->begin, out->end, &total)) != DGREP_OK) {
       dgrep_partitions_free(out);
       return rc;

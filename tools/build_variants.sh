@@ -1,0 +1,30 @@
+#!/bin/bash
+# Build tuning variants of the scan kernels in parallel (the sequential
+# `make variants` takes ~2.5 min per variant):
+#   tools/build_variants.sh 'name=-DKNOB=1 -DOTHER=2' 'name2=...' ...
+# Writes distributed-grep_amd/variants/libdgrep_<name>.so (run with
+# DGREP_LIB=...; tools/variant_bench.sh). The other objects come from the
+# normal build, which must be current (make -C distributed-grep_amd).
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+P=$R/distributed-grep_amd
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function"
+mkdir -p "$P/variants" "$P/build"
+make -s -C "$P" >/dev/null
+pids=()
+for spec in "$@"; do
+  name=${spec%%=*}
+  defs=${spec#*=}
+  (
+    $HIPCC $FLAGS $defs -c "$P/csrc/kernels/scan_dfa.hip" -o "$P/build/scan_dfa_$name.o" 2> "$P/build/variant_$name.log" &&
+      $HIPCC -shared -fPIC --offload-arch=gfx950 -o "$P/variants/libdgrep_$name.so" \
+        "$P"/build/go_parser.o "$P"/build/dfa_builder.o "$P"/build/compile_api.o "$P/build/scan_dfa_$name.o" \
+        "$P"/build/encode.o "$P"/build/reduce.o "$P"/build/dgrep_runtime.o "$P"/build/build_info.o &&
+      echo "built $name ($defs)"
+  ) &
+  pids+=($!)
+done
+rc=0
+for p in "${pids[@]}"; do wait "$p" || rc=1; done
+exit $rc
