@@ -164,7 +164,8 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
     uint32_t lo = sw[0];
     for (uint64_t k = 0; k < nd; ++k) {
       const uint32_t hi = sw[k + 1];
-      dw[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh * 8u) : lo;
+      // v_alignbyte_b32 takes the shift in BYTES: ({hi, lo} >> 8 * sh)[31:0]
+      dw[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
       lo = hi;
     }
     i += nd * 4;
