@@ -17,10 +17,12 @@ for spec in "$@"; do
   name=${spec%%=*}
   defs=${spec#*=}
   (
+    # the runtime builds the LDS images, so it takes the same knobs
     $HIPCC $FLAGS $defs -c "$P/csrc/kernels/scan_dfa.hip" -o "$P/build/scan_dfa_$name.o" 2> "$P/build/variant_$name.log" &&
+      $HIPCC $FLAGS $defs -c "$P/csrc/runtime/dgrep_runtime.hip" -o "$P/build/dgrep_runtime_$name.o" 2>> "$P/build/variant_$name.log" &&
       $HIPCC -shared -fPIC --offload-arch=gfx950 -o "$P/variants/libdgrep_$name.so" \
         "$P"/build/go_parser.o "$P"/build/dfa_builder.o "$P"/build/compile_api.o "$P/build/scan_dfa_$name.o" \
-        "$P"/build/encode.o "$P"/build/reduce.o "$P"/build/dgrep_runtime.o "$P"/build/build_info.o &&
+        "$P"/build/encode.o "$P"/build/reduce.o "$P/build/dgrep_runtime_$name.o" "$P"/build/build_info.o &&
       echo "built $name ($defs)"
   ) &
   pids+=($!)
