@@ -86,19 +86,6 @@ constexpr uint32_t kCandidateBit = 0x80000000u;
 enum : uint32_t { kStatusLineTooLong = 1u, kStatusCandidateTooLong = 2u };
 
 constexpr int kScanThreads = 256;  // 4 waves per workgroup
-
-// StepSheng8's LDS image. DGREP_SHENG_LP = 1: LANE-PRIVATE banks -- V[b] (8
-// bytes) is stored 32 times, copy j at b * 256 + 8 * j, and lane l reads copy
-// l % 32, so its ds_read_b64 always hits banks 2j, 2j+1 (mod 64) whatever the
-// byte: a wave's V reads never conflict (the shared 2 KiB table at 8 * b spent
-// 55 % of its LDS cycles on conflicts over log text, tools/lds_bank_bench.hip).
-// The 64 KiB image is shared by one 768-thread workgroup per CU (3 waves per
-// SIMD, as before), with kShengLpSlots LDS record slots per lane.
-#ifndef DGREP_SHENG_LP
-#define DGREP_SHENG_LP 0
-#endif
-constexpr uint32_t kShengImageBytes = DGREP_SHENG_LP ? 65536 : 2048;
-constexpr int kShengThreads = DGREP_SHENG_LP ? 768 : kScanThreads;
 constexpr int kTileLanes = 64;     // a tile is one wave's 64 chunks
 
 // DFA stepper selected by dgrep_load_dfa from the state count.
@@ -110,7 +97,8 @@ enum : int {
   kStepFilter = 4,  // > 256 states: the DFA's shallow part in LDS, lines that leave it verified afterwards
 };
 
-// LDS image of kStepFilter: u8 classes [256], then u16 [state][class] rows of the
+// LDS image of kStepFilter: byte classes [256] (u8, or u32 with
+// DGREP_FILTER_CLS32), then u16 [state][class] rows of the
 // filter DFA (its states premultiplied by the class count), at most this many
 // bytes in all -- with 1024 threads x 4 slots x 8 B the workgroup stays within
 // the CU's 160 KiB.
@@ -118,18 +106,26 @@ enum : int {
 #define DGREP_FILTER_KIB 124
 #endif
 constexpr uint32_t kFilterImageBytes = DGREP_FILTER_KIB * 1024;
-// u8 classes: four byte values share a dword, so the printable ASCII range
-// (0x20-0x7f) spans 24 dwords in 24 distinct banks and a wave's class reads of
-// text never conflict (tools/lds_bank_bench.hip: u8 0 % conflict cycles, u32
-// entries at 4*b 52 %, u64 at 8*b 55 %)
-constexpr uint32_t kFilterClassBytes = 256;
+// u8 classes: four byte values share a dword, so printable ASCII (0x20-0x7f)
+// spans 24 dwords in 24 distinct banks and a wave's class reads of text never
+// conflict (tools/lds_bank_bench.hip on the log corpus: u8 table 0 % conflict
+// cycles, u32 entries at 4*b 52 %, u64 at 8*b 55 %). C4 kernel 3.18 -> 3.38 TB/s.
+#ifndef DGREP_FILTER_CLS32
+#define DGREP_FILTER_CLS32 0
+#endif
+constexpr uint32_t kFilterClassBytes = DGREP_FILTER_CLS32 ? 1024 : 256;
 
 // StepPair's two-byte table T2 (u16 [state][class][class], premultiplied
 // states) must address itself with 16-bit values; its whole LDS image (T2 +
-// T1 + the 256-byte class table) at most kPairMaxImage bytes.
+// T1 + the 1 KiB byte table) at most kPairMaxImage bytes.
 constexpr uint32_t kPairMaxT2 = 32768;
 constexpr uint32_t kPairMaxImage = 40960;
-constexpr uint32_t kPairT2 = 256;  // LDS address of T2 (after the u8 class table)
+// DGREP_PAIR_U8: one u8 class table CL[b] = 2*class(b) (256 B, conflict-free
+// over text) and a v_mad_u32_u24 per pair, instead of the u32 UA/UB tables.
+#ifndef DGREP_PAIR_U8
+#define DGREP_PAIR_U8 0
+#endif
+constexpr uint32_t kPairT2 = DGREP_PAIR_U8 ? 256 : 2048;  // LDS address of T2 (after the byte tables)
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
 // runtime renumbers states hottest-first (start, start_m, then BFS order from

@@ -57,7 +57,7 @@
 #define DGREP_SHENG_CHUNK 4096
 #endif
 #ifndef DGREP_SHENG_SLOTS
-#define DGREP_SHENG_SLOTS (DGREP_SHENG_LP ? 8 : 16)
+#define DGREP_SHENG_SLOTS 24
 #endif
 #ifndef DGREP_SHENG_BLOCK
 #define DGREP_SHENG_BLOCK 128
@@ -69,7 +69,7 @@
 #define DGREP_TABLE_CHUNK 2048
 #endif
 #ifndef DGREP_TABLE_SLOTS
-#define DGREP_TABLE_SLOTS 8
+#define DGREP_TABLE_SLOTS 6
 #endif
 #ifndef DGREP_TABLE_STAGING
 #define DGREP_TABLE_STAGING 0
@@ -166,7 +166,7 @@ constexpr uint32_t kRow = 260;
 template <int TBL, int E, int NT>
 struct ScanSmem {
   alignas(16) uint8_t tbl[TBL];  // first member: the table sits at LDS address 0
-  uint2 slots[NT * E];           // record slot i of thread t (stream k): [(i * S + k) * NT + t]
+  uint32_t slots[NT * E * 2];
 };
 
 // DFA of at most 256 states: u8 transition table, row s at LDS s*260.
@@ -196,30 +196,18 @@ struct StepTable {
 // DFA of at most 8 states (Sheng-style): V[b] = 8 next-state bytes. Only byte
 // 0 of the carried state is meaningful; v_perm fills bytes 1-3 with other
 // (valid, < 8) states, which never reach byte 0 of a later result.
-// DGREP_SHENG_LP: V[b] for this lane sits at b * 256 + lp (lp = 8 * (lane % 32),
-// see kShengImageBytes); one v_perm builds that address from the input word.
 struct StepSheng8 {
   static constexpr int kKind = kStepSheng8;
-  const uint8_t* V;
-  uint32_t lp;  // lane-private byte offset (DGREP_SHENG_LP), else 0
+  const uint2* V;
   __device__ __forceinline__ static uint32_t sel(const uint2 v, uint32_t s) {
     return __builtin_amdgcn_perm(v.y, v.x, s);
   }
-  // LDS address of V[byte k of x]
-  template <int K>
-  __device__ __forceinline__ uint32_t addr(uint32_t x) const {
-    if constexpr (DGREP_SHENG_LP)
-      return __builtin_amdgcn_perm(x, lp, 0x0c0c0000u | ((4u + K) << 8));  // (byte_k << 8) | lp
-    else
-      return ((x >> (8 * K)) & 0xffu) * 8u;
-  }
-  __device__ __forceinline__ uint2 at(uint32_t off) const { return *reinterpret_cast<const uint2*>(V + off); }
   // the four LDS reads depend only on the input word: issued a word ahead
   struct Pre {
     uint2 m0, m1, m2, m3;
   };
   __device__ __forceinline__ Pre prep(uint32_t x) const {
-    return Pre{at(addr<0>(x)), at(addr<1>(x)), at(addr<2>(x)), at(addr<3>(x))};
+    return Pre{V[x & 0xffu], V[(x >> 8) & 0xffu], V[(x >> 16) & 0xffu], V[x >> 24]};
   }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
@@ -228,7 +216,7 @@ struct StepSheng8 {
     s2 = sel(p.m2, s1);
     s3 = sel(p.m3, s2);
   }
-  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(at(addr<0>(b)), s); }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[b], s); }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return (s & 0xffu) == M; }
   // states are replicated bytes and start_m is the highest state (host
   // renumbering): one max over the word's four states replaces four compares
@@ -288,15 +276,15 @@ struct StepWide {
 
 // DFA whose two-byte table fits in LDS (2 * S' * K^2 <= kPairMaxT2 bytes; C3's
 // 20-state, 12-class regex: 6 KiB): ONE table lookup per TWO input bytes.
-// LDS image (a 256-byte class table first, at LDS address 0):
-//   CL (u8 [256]): CL[b] = 2*class(b); a pair's column offset 2*(c1*K + c2) =
-//      CL[b0]*K + CL[b1] (one v_mad_u32_u24); the lookups depend only on the
-//      input and are issued a word ahead. u8 entries: four byte values share a
-//      dword, so text's class reads are bank-conflict-free (the r02 u32 tables
-//      at 4*b spent 48 % of the LDS cycles on conflicts);
+// LDS image (kPairT2 = 2 KiB of byte tables first, at LDS address 0):
+//   UA, UB (u32 [256] each): UA[b] = 2K*class(b), UB[b] = 2*class(b), so the
+//      pair's column offset 2*(c1*K + c2) = UA[b0] + UB[b1]; the four lookups
+//      of a word share one address (4*b, UB by the instruction's immediate
+//      offset), depend only on the input and are issued a word ahead; u32
+//      entries put byte b in bank b % 32 (text spreads over the banks);
 //   T2 (at kPairT2): u16 [S'][K][K], entry = next state after the pair,
 //      PREMULTIPLIED to its row's LDS address (kPairT2 + id * 2K^2), so the
-//      dependent chain per pair is one v_add + one ds_read_u16;
+//      dependent chain per pair is one v_add3 + one ds_read_u16;
 //   T1: u16 [S'][K] premultiplied single-byte steps (split tail, last-line check).
 // A pair hides the state between its two bytes, so a '\n' FIRST in a pair that
 // ends a matching line (the byte enters start_m) leads to a SHADOW state: a copy
@@ -310,26 +298,36 @@ struct StepPair {
   const uint16_t* T1;
   uint32_t thr, M, div, K;
   struct Pre {
-    uint32_t a0, a2;
+    uint32_t a0, b1, a2, b3;
   };
-  __device__ __forceinline__ uint32_t cl(uint32_t b) const { return lds[b]; }
+  __device__ __forceinline__ uint32_t ua(uint32_t b) const {
+    return *reinterpret_cast<const uint32_t*>(lds + 4u * b);
+  }
+  __device__ __forceinline__ uint32_t ub(uint32_t b) const {
+    if constexpr (DGREP_PAIR_U8) return lds[b];  // CL[b] = 2 * class(b)
+    return *reinterpret_cast<const uint32_t*>(lds + 1024u + 4u * b);
+  }
   __device__ __forceinline__ Pre prep(uint32_t x) const {
-    const uint32_t c0 = cl(x & 0xffu), c1 = cl((x >> 8) & 0xffu), c2 = cl((x >> 16) & 0xffu), c3 = cl(x >> 24);
-    return Pre{__umul24(c0, K) + c1, __umul24(c2, K) + c3};
+    if constexpr (DGREP_PAIR_U8) {
+      // a0 = 2K*c0 + 2*c1, a2 = 2K*c2 + 2*c3 (b1 = b3 = 0)
+      const uint32_t c0 = lds[x & 0xffu], c1 = lds[(x >> 8) & 0xffu], c2 = lds[(x >> 16) & 0xffu], c3 = lds[x >> 24];
+      return Pre{__umul24(c0, K) + c1, 0u, __umul24(c2, K) + c3, 0u};
+    }
+    return Pre{ua(x & 0xffu), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu), ub(x >> 24)};
   }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
     return *reinterpret_cast<const uint16_t*>(lds + off);
   }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
-    s1 = t2(s + p.a0);
-    s3 = t2(s1 + p.a2);
+    s1 = t2(s + p.a0 + p.b1);
+    s3 = t2(s1 + p.a2 + p.b3);
     s0 = s1;
     s2 = s3;
   }
   // single-byte step (rare paths): state id = (premultiplied state - kPairT2) / row bytes
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-    return T1[((s - kPairT2) / div) * K + (cl(b) >> 1)];
+    return T1[((s - kPairT2) / div) * K + (ub(b) >> 1)];
   }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
   __device__ __forceinline__ bool any2(uint32_t s1, uint32_t s3) const { return max(s1, s3) >= thr; }
@@ -350,7 +348,7 @@ struct StepPair {
 // it on the whole DFA. For C4's 1,000 keywords the shallow part is depth <= 3
 // of the Aho-Corasick-like DFA and 0.8 % of the lines are candidates.
 // LDS: the byte classes as u8 [256] (four byte values per dword: text's class
-// reads are bank-conflict-free, see kFilterClassBytes), then u16 [state][class] rows, entries premultiplied by the class count (entry
+// reads never conflict, see kFilterClassBytes), then u16 [state][class] rows, entries premultiplied by the class count (entry
 // index of the next state's row): the dependent chain per byte is one
 // v_add_lshl + one ds_read_u16; the class lookups depend only on the input and
 // are issued a word ahead. Ids: shallow states, CAND, start_m, CAND_END -- an
@@ -362,7 +360,10 @@ struct StepFilter {
   struct Pre {
     uint32_t c0, c1, c2, c3;
   };
-  __device__ __forceinline__ uint32_t cls(uint32_t b) const { return lds[b]; }
+  __device__ __forceinline__ uint32_t cls(uint32_t b) const {
+    if constexpr (DGREP_FILTER_CLS32) return *reinterpret_cast<const uint32_t*>(lds + 4u * b);
+    return lds[b];  // u8: see kFilterClassBytes
+  }
   __device__ __forceinline__ Pre prep(uint32_t x) const {
     return Pre{cls(x & 0xffu), cls((x >> 8) & 0xffu), cls((x >> 16) & 0xffu), cls(x >> 24)};
   }
@@ -402,7 +403,7 @@ template <>
 __device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }
 template <>
 __device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds, const ScanArgs&) {
-  return StepSheng8{lds, DGREP_SHENG_LP ? 8u * (threadIdx.x & 31u) : 0u};
+  return StepSheng8{reinterpret_cast<const uint2*>(lds)};
 }
 template <>
 __device__ __forceinline__ StepWide make_step<StepWide>(const uint8_t* lds, const ScanArgs& a) {
@@ -455,13 +456,6 @@ constexpr int streams_of() {
   return Step::kKind == kStepTable ? (TBL <= 64 * int(kRow) ? Tune<Step>::S : 1) : Tune<Step>::S;
 }
 
-// LDS record slots per lane: the 256-state u8 table (65 KiB) keeps two
-// workgroups per CU with 4
-template <class Step, int TBL>
-constexpr int slots_of() {
-  return Step::kKind == kStepTable && TBL > 128 * int(kRow) ? 4 : Tune<Step>::E;
-}
-
 // Per-lane run state. Positions are relative to the lane's chunk start `cs`.
 struct LaneRun {
   uint32_t s;        // DFA state
@@ -478,37 +472,16 @@ struct LaneRun {
   int32_t p1;
 };
 
-// Records of matching lines. DIRECT (overflow pass): straight to the staging
-// buffer. Slot mode: a RING of E (a power of two) LDS slots per lane, slot i at
-// slots[i * ST] (ST = threads x streams: slot i of consecutive lanes are
-// consecutive 8-byte words, so the lanes of a write never share a bank). A
-// record is written to slot nev % E unconditionally -- a non-record (ok ==
-// false) lands in the next free slot and is not counted -- so the common event
-// path has no branch; when the ring fills (nev % E == 0 after a record) it is
-// copied to the lane's HBM spill area (rare, once per E records). At the
-// tile's end records [0, F) come from the spill area (F = nev / E * E) and the
-// rest from the ring. Capacity: F <= spill_cap, or nev < E with no spill area
-// (a full ring has nowhere to go before the next write would reuse slot 0).
-template <int E, bool DIRECT, int ST>
+template <int E, bool DIRECT>
 struct Emitter {
-  static_assert(DIRECT || (E > 0 && (E & (E - 1)) == 0), "LDS slot ring: E must be a power of two");
   const ScanArgs* a;
-  uint2* slots;          // this lane's slot 0 (slot mode)
+  uint32_t* slots;       // LDS [E][2] of this lane (slot mode)
   uint64_t cs;
   uint64_t out_base;     // first staging index of this lane (direct mode)
   uint32_t nl_prefix;    // '\n' between tile start and chunk start (direct mode)
   uint2* spill = nullptr;    // slot mode: this lane's HBM spill area (nullptr: none)
   uint32_t spill_cap = 0;    // its records
 
-  __device__ __forceinline__ void put(LaneRun& r, uint32_t w0, uint32_t lw, bool ok) const {
-    slots[(r.nev % uint32_t(E)) * ST] = make_uint2(w0, lw);
-    r.nev += ok ? 1u : 0u;
-    if (ok && (r.nev % uint32_t(E)) == 0u && spill && r.nev <= spill_cap) {
-      // the ring is full: its E records move to spill[nev - E, nev)
-#pragma unroll
-      for (int i = 0; i < E; ++i) spill[r.nev - uint32_t(E) + uint32_t(i)] = slots[i * ST];
-    }
-  }
   // cand: a filter candidate (kCandidateBit in len, verified afterwards)
   __device__ __forceinline__ void operator()(LaneRun& r, uint64_t q, int64_t start, uint32_t rel,
                                              bool cand = false) const {
@@ -523,22 +496,28 @@ struct Emitter {
         L.rel = nl_prefix + rel;
         a->staging[o] = L;
       }
-      ++r.nev;
     } else {
       // start < C and rel < C fit 16 bits each
-      put(r, uint32_t(start) | (rel << 16), lw, true);
+      const uint32_t w0 = uint32_t(start) | (rel << 16);
+      if (r.nev < uint32_t(E)) {
+        slots[r.nev * 2 + 0] = w0;
+        slots[r.nev * 2 + 1] = lw;
+      } else if (r.nev - uint32_t(E) < spill_cap) {
+        // LDS slots full: the lane's further records go to its spill area in
+        // HBM (read back at the tile's end), so a dense pattern neither caps
+        // the lane chunk nor sends the lane to the overflow pass
+        spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
+      }
     }
     if (len > 0xffffffffull) atomicOr(a->status, kStatusLineTooLong);
     if (cand && len >= uint64_t(kCandidateBit)) atomicOr(a->status, kStatusCandidateTooLong);
+    ++r.nev;
   }
   // The same for a line wholly inside the lane's chunk (start < q < C <= 32 KiB):
-  // 32-bit chunk-relative positions, no length checks; ok == false: not a
-  // record (the lane has not crossed a line boundary yet).
-  __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand,
-                                        bool ok) const {
+  // 32-bit chunk-relative positions, no length checks.
+  __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
     const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
     if (DIRECT) {
-      if (!ok) return;
       const uint64_t o = out_base + r.nev;
       if (o < a->capacity) {
         StagedLine L;
@@ -547,21 +526,16 @@ struct Emitter {
         L.rel = nl_prefix + rel;
         a->staging[o] = L;
       }
-      ++r.nev;
     } else {
-      put(r, start | (rel << 16), lw, ok);
+      const uint32_t w0 = start | (rel << 16);
+      if (r.nev < uint32_t(E)) {
+        slots[r.nev * 2 + 0] = w0;
+        slots[r.nev * 2 + 1] = lw;
+      } else if (r.nev - uint32_t(E) < spill_cap) {
+        spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
+      }
     }
-  }
-  // slot mode, at the tile's end: records in the spill area, and whether every
-  // record was kept (else the lane goes to the overflow pass)
-  __device__ __forceinline__ uint32_t spilled(const LaneRun& r) const {
-    return spill ? r.nev / uint32_t(E) * uint32_t(E) : 0u;
-  }
-  __device__ __forceinline__ bool kept_all(const LaneRun& r) const {
-    return spill ? spilled(r) <= spill_cap : r.nev < uint32_t(E);
-  }
-  __device__ __forceinline__ uint2 record(const LaneRun& r, uint32_t j) const {
-    return j < spilled(r) ? spill[j] : slots[(j % uint32_t(E)) * ST];
+    ++r.nev;
   }
 };
 
@@ -577,14 +551,14 @@ struct Blk {
 
 // Everything a word step does after its four DFA steps s0..s3 (newline mask
 // m): matching-line events, the first-piece map (TRACK), newline bookkeeping.
-template <int J, bool TRACK, class Step, int E, bool DIRECT, int ST>
+template <int J, bool TRACK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
                                             uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
-                                            const Emitter<E, DIRECT, ST>& emit);
+                                            const Emitter<E, DIRECT>& emit);
 
-template <int J, bool TRACK, class Step, int E, bool DIRECT, int ST>
+template <int J, bool TRACK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x, const typename Step::Pre& pre,
-                                          uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT, ST>& emit) {
+                                          uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   // StepTable: keep each word's work in place (hoisting the chain-independent
   // newline masks of a whole block costs ~100 VGPRs). StepSheng8 wants the
   // opposite: its state-independent LDS reads should run ahead of the chain.
@@ -599,11 +573,11 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
 
 // Two independent chunks per lane stepped in lockstep: both dependency chains
 // are in one basic block (events come after both), so their latencies overlap.
-template <int J, class Step, int E, bool DIRECT, int ST>
+template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_step2(const Step& st, uint32_t M, uint32_t xa, uint32_t xb,
                                            const typename Step::Pre& pa, const typename Step::Pre& pb, uint32_t& sa,
                                            uint32_t& sb, Blk& ba, Blk& bb, LaneRun& ra, LaneRun& rb,
-                                           const Emitter<E, DIRECT, ST>& ea, const Emitter<E, DIRECT, ST>& eb) {
+                                           const Emitter<E, DIRECT>& ea, const Emitter<E, DIRECT>& eb) {
   __builtin_amdgcn_sched_barrier(0);
   const uint32_t ma = nl_mask(xa), mb = nl_mask(xb);
   uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
@@ -636,17 +610,17 @@ __device__ __forceinline__ bool word_any(const Step& st, uint32_t M, uint32_t s0
 // the previous '\n' (an earlier word of the block, or r.prev_nl), all positions
 // are chunk-relative 32-bit values. Anything else (several '\n' in one word,
 // the part past the chunk end) takes the general loop.
-template <int J, class Step, int E, bool DIRECT, int ST>
+template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                           uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
-                                          const Emitter<E, DIRECT, ST>& emit) {
+                                          const Emitter<E, DIRECT>& emit) {
   if (!b.past && (m & (m - 1u)) == 0u) {
     // branch-free operands (selects, no nested exec-mask regions)
     const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
     const uint32_t lastpos = uint32_t(b.pos) + 4u * uint32_t(b.lastj) + hi_byte(b.lastm | 1u);
     const uint32_t prev = b.lastm ? lastpos : uint32_t(r.prev_nl);
     const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
-    emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk), r.seen | (b.lastm != 0));
+    if (r.seen | (b.lastm != 0)) emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk));
     return;
   }
   const uint64_t q0 = b.pos + 4u * J;
@@ -679,10 +653,10 @@ __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
   if (m) { b.lastm = m; b.lastj = J; }
 }
 
-template <int J, bool TRACK, class Step, int E, bool DIRECT, int ST>
+template <int J, bool TRACK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
                                             uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
-                                            const Emitter<E, DIRECT, ST>& emit) {
+                                            const Emitter<E, DIRECT>& emit) {
   if (__builtin_expect(word_any(st, M, s0, s1, s2, s3), 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
   if constexpr (TRACK) {
     if (r.p1 < 0) {
@@ -701,10 +675,10 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
 // each with the bookkeeping of the words before it -- then the newline
 // bookkeeping. The event branch is entered once per 16 bytes instead of once
 // per word that holds an event in any of the wave's 64 lanes.
-template <int J, int NW, class Step, int E, bool DIRECT, int ST>
+template <int J, int NW, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void quad_step(const Step& st, uint32_t M, const uint32_t (&w)[NW],
                                           typename Step::Pre& pre, uint32_t& s, Blk& b, LaneRun& r,
-                                          const Emitter<E, DIRECT, ST>& emit) {
+                                          const Emitter<E, DIRECT>& emit) {
   uint32_t q[4][4], m[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -752,10 +726,10 @@ __device__ __forceinline__ void blk_finish(const Blk& b, uint32_t s, LaneRun& r)
 }
 
 // One BK-byte block of each of a lane's two chunks (see word_step2).
-template <int BK, class Step, int E, bool DIRECT, int ST>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uint4 (&va)[BK / 16],
                                            const uint4 (&vb)[BK / 16], uint64_t pos, uint64_t C, LaneRun& ra,
-                                           LaneRun& rb, const Emitter<E, DIRECT, ST>& ea, const Emitter<E, DIRECT, ST>& eb) {
+                                           LaneRun& rb, const Emitter<E, DIRECT>& ea, const Emitter<E, DIRECT>& eb) {
   Blk ba, bb;
   blk_init(ba, pos, C, ra);
   blk_init(bb, pos, C, rb);
@@ -806,9 +780,9 @@ constexpr bool use_quads() {
          Step::kKind == kStepPair;
 }
 
-template <int BK, bool TRACK = false, class Step, int E, bool DIRECT, int ST>
+template <int BK, bool TRACK = false, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
-                                          uint64_t C, LaneRun& r, const Emitter<E, DIRECT, ST>& emit) {
+                                          uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
   blk_init(b, pos, C, r);
   uint32_t s = r.s;
@@ -868,9 +842,9 @@ constexpr bool nt_loads() {
 
 // The last < BLOCK bytes of the split, one byte at a time, then the end of the
 // split closes the last owned line (strings.Split's final piece).
-template <class Step, int E, bool DIRECT, int ST>
+template <class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8_t* p, uint64_t pos, uint64_t avail, uint64_t C,
-                         LaneRun& r, uint32_t& nl_chunk, bool& snap, const Emitter<E, DIRECT, ST>& emit) {
+                         LaneRun& r, uint32_t& nl_chunk, bool& snap, const Emitter<E, DIRECT>& emit) {
   for (; pos < avail; ++pos) {
     if (pos == C) { nl_chunk = r.nl; snap = true; }
     if (pos >= C && r.term) return;
@@ -905,9 +879,9 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
 // BK-byte blocks with direct per-lane loads, prefetching the next block while
 // the current one is stepped (two register buffers, ping-pong). Returns the
 // number of '\n' inside the lane's own chunk [cs, cs + C).
-template <int BK, class Step, int E, bool DIRECT, int ST>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step& st, uint64_t cs, uint64_t pos0,
-                                                  LaneRun& r, const Emitter<E, DIRECT, ST>& emit, const uint32_t C) {
+                                                  LaneRun& r, const Emitter<E, DIRECT>& emit, const uint32_t C) {
   const uint32_t M = a.start_m;
   const uint64_t avail = cs < a.n ? a.n - cs : 0;
   if (avail <= pos0) {
@@ -941,9 +915,9 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   return nl_chunk;
 }
 
-template <int BK, class Step, int E, bool DIRECT, int ST>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
-                                             const Emitter<E, DIRECT, ST>& emit, const uint32_t C) {
+                                             const Emitter<E, DIRECT>& emit, const uint32_t C) {
   lane_init(a, cs, r);
   if (cs >= a.n) return 0;
   return run_lane_from<BK>(a, st, cs, 0, r, emit, C);
@@ -952,9 +926,9 @@ __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, 
 // Two chunks per lane (csa, csb), both wholly inside the split, stepped in
 // lockstep over [0, C) with direct loads (two independent dependency chains
 // per lane); then each finishes its last owned line on its own.
-template <int C, int BK, class Step, int E, int ST>
+template <int C, int BK, class Step, int E>
 __device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uint64_t csa, uint64_t csb, LaneRun& ra,
-                                          LaneRun& rb, const Emitter<E, false, ST>& ea, const Emitter<E, false, ST>& eb,
+                                          LaneRun& rb, const Emitter<E, false>& ea, const Emitter<E, false>& eb,
                                           uint32_t& nla, uint32_t& nlb) {
   static_assert(C % (2 * BK) == 0, "chunk must hold an even number of blocks");
   const uint32_t M = a.start_m;
@@ -998,9 +972,9 @@ __device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* lds) {
 // lane's ds_read_b128 of its piece j bank-conflict-free. One ring per wave:
 // the next round is issued as soon as the lane holds its pieces. After the
 // chunk, the lane finishes its last owned line with direct loads.
-template <int C, int R, class Step, int E, int ST>
+template <int C, int R, class Step, int E>
 __device__ __forceinline__ uint32_t run_lane_staged(const ScanArgs& a, const Step& st, uint64_t cs, int lane,
-                                                    uint8_t* stage, LaneRun& r, const Emitter<E, false, ST>& emit) {
+                                                    uint8_t* stage, LaneRun& r, const Emitter<E, false>& emit) {
   constexpr int P = R / 16, SPI = 64 / P, G = 16 / P, NR = C / R;
   static_assert(P * SPI == 64 && C % R == 0, "bad staging shape");
   lane_init(a, cs, r);
@@ -1114,7 +1088,7 @@ constexpr int waves_per_simd() {
 
 template <class Step, int TBL, int NT>
 __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(ScanArgs a) {
-  constexpr int E = slots_of<Step, TBL>(), BK = Tune<Step>::B;
+  constexpr int E = Tune<Step>::E, BK = Tune<Step>::B;
   constexpr bool kStaged = use_staging<Step, TBL>();
   const uint32_t C = lane_chunk<Step, TBL>(a);
   constexpr int R = DGREP_STAGE_ROUND;
@@ -1130,8 +1104,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
 
   const Step st = make_step<Step>(sm.tbl, a);
   constexpr int S = streams_of<Step, TBL>();  // chunks per lane: chunk k of a tile is k * 64 + lane
-  constexpr int ST = S * NT;  // slot stride (Emitter)
-  uint2* slots = sm.slots + tid;
+  uint32_t* slots = sm.slots + tid * S * E * 2;
   const int lane = tid & 63;
   const uint64_t waves = uint64_t(gridDim.x) * (NT / 64);
   const uint64_t kTile = uint64_t(kTileLanes) * uint64_t(S) * uint64_t(C);
@@ -1142,32 +1115,28 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
 #pragma unroll
     for (int k = 0; k < S; ++k) cs[k] = t * kTile + (uint64_t(k) * kTileLanes + uint64_t(lane)) * uint64_t(C);
     const bool full = (t + 1) * kTile <= a.n;  // wave-uniform: the whole tile lies inside the split
-    Emitter<E, false, ST> em[S];
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
-      em[k] = Emitter<E, false, ST>{&a, slots + k * NT, cs[k], 0, 0};
-      if (S == 1 && a.spill) {
-        // the one-chunk-per-lane steppers' HBM spill area
-        em[k].spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane;
-        em[k].spill_cap = a.spill_per_lane;
-      }
-    }
     if constexpr (S == 2) {
+      const Emitter<E, false> e0{&a, slots, cs[0], 0, 0}, e1{&a, slots + E * 2, cs[1], 0, 0};
       if (full) {
-        run_lane2<Tune<Step>::C, BK>(a, st, cs[0], cs[1], r[0], r[1], em[0], em[S - 1], nlc[0], nlc[S - 1]);
+        run_lane2<Tune<Step>::C, BK>(a, st, cs[0], cs[1], r[0], r[1], e0, e1, nlc[0], nlc[1]);
       } else {
-        nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em[0], C);
-        nlc[S - 1] = run_lane<BK>(a, st, cs[S - 1], r[S - 1], em[S - 1], C);
+        nlc[0] = run_lane<BK>(a, st, cs[0], r[0], e0, C);
+        nlc[1] = run_lane<BK>(a, st, cs[1], r[1], e1, C);
       }
     } else {
+      Emitter<E, false> em{&a, slots, cs[0], 0, 0};
+      if (a.spill) {
+        em.spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane;
+        em.spill_cap = a.spill_per_lane;
+      }
       if constexpr (kStaged) {
         if (full)
-          nlc[0] = run_lane_staged<Tune<Step>::C, R>(a, st, cs[0], lane, stage + (tid >> 6) * (DGREP_STAGE_DEPTH * 64 * R),
-                                                     r[0], em[0]);
+          nlc[0] = run_lane_staged<Tune<Step>::C, R>(a, st, cs[0], lane, stage + (tid >> 6) * (DGREP_STAGE_DEPTH * 64 * R), r[0],
+                                         em);
         else
-          nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em[0], C);
+          nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
       } else {
-        nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em[0], C);
+        nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
       }
     }
 
@@ -1197,16 +1166,27 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const uint32_t nev = r[k].nev;
+      const uint32_t* sl = slots + k * E * 2;
+      const bool spill = S == 1 && a.spill;
+      const uint2* sp = spill ? a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane : nullptr;
       const uint64_t o0 = base + ev_off[k];
-      if (em[k].kept_all(r[k])) {
+      if (nev <= uint32_t(E) + (spill ? a.spill_per_lane : 0u)) {
         for (uint32_t j = 0; j < nev; ++j) {
           const uint64_t o = o0 + j;
           if (o < a.capacity) {
-            const uint2 w = em[k].record(r[k], j);
+            uint32_t w0, w1;
+            if (j < uint32_t(E)) {
+              w0 = sl[j * 2 + 0];
+              w1 = sl[j * 2 + 1];
+            } else {
+              const uint2 w = sp[j - uint32_t(E)];
+              w0 = w.x;
+              w1 = w.y;
+            }
             StagedLine L;
-            L.start = cs[k] + (w.x & 0xffffu);
-            L.len = w.y;
-            L.rel = nl_off[k] + (w.x >> 16);
+            L.start = cs[k] + (w0 & 0xffffu);
+            L.len = w1;
+            L.rel = nl_off[k] + (w0 >> 16);
             a.staging[o] = L;
           }
         }
@@ -1261,14 +1241,14 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
     uint32_t nl = 0, nev = 0;
     if (live) {
       // out_base = capacity: every write of the counting pass is skipped
-      Emitter<E, true, 1> cnt{&a, nullptr, cs, a.capacity, 0};
+      Emitter<E, true> cnt{&a, nullptr, cs, a.capacity, 0};
       nl = run_lane<BK>(a, st, cs, r, cnt, len);
       nev = r.nev;
     }
     const uint32_t nl_off = wave_incl_scan(nl) - nl;
     const uint32_t ev_off = wave_incl_scan(nev) - nev;
     if (live && nev) {
-      Emitter<E, true, 1> ed{&a, nullptr, cs, ol.out_base + ev_off, ol.nl_prefix + nl_off};
+      Emitter<E, true> ed{&a, nullptr, cs, ol.out_base + ev_off, ol.nl_prefix + nl_off};
       run_lane<BK>(a, st, cs, r, ed, len);
     }
   }
@@ -1456,10 +1436,7 @@ uint32_t scan_table_row() { return kRow; }
 namespace {
 template <class Step>
 constexpr int threads_of() {
-  return Step::kKind == kStepWide     ? kWideThreads
-         : Step::kKind == kStepFilter ? kFilterThreads
-         : Step::kKind == kStepSheng8 ? kShengThreads
-                                      : kScanThreads;
+  return Step::kKind == kStepWide ? kWideThreads : Step::kKind == kStepFilter ? kFilterThreads : kScanThreads;
 }
 template <class Step, int TBL>
 hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
@@ -1484,7 +1461,7 @@ hipError_t occ_t(int* b) {
 // One switch for every entry point: stepper by kind, LDS image by size.
 template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
-  if (kind == kStepSheng8) return op.template run<StepSheng8, int(kShengImageBytes)>();
+  if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
   if (kind == kStepPair) {
     if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
     if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
@@ -1531,7 +1508,7 @@ struct TileOp {
     uint64_t c = uint64_t(Tune<S>::C);
     // a lane's record capacity: its LDS slots, plus the HBM spill area of the
     // one-chunk-per-lane steppers
-    constexpr uint32_t E = uint32_t(slots_of<S, T>());
+    constexpr uint32_t E = uint32_t(Tune<S>::E);
     const uint32_t cap = E + (adaptive_chunk<S, T>() ? spill_per_lane : 0u);
     *slots = cap;
     // at most a quarter of the capacity expected in use: an overflowing lane

@@ -180,7 +180,7 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 }
 
 // The pair stepper's LDS image (StepPair, scan_dfa.hip) from the blob's DFA:
-// CL u8 [256] (2 * byte class), T2 u16 [S'][K][K] at kPairT2 (two
+// UA, UB u32 [256] (byte -> column offsets), T2 u16 [S'][K][K] at kPairT2 (two
 // bytes per lookup), T1 u16 [S'][K] (single bytes); states premultiplied to
 // their T2 row's LDS address (kPairT2 + id * 2K^2). S' = S + shadows: a pair whose FIRST byte is a '\n'
 // entering start_m hides that event in the state between its bytes, so it
@@ -205,7 +205,7 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
     }
   const uint32_t Sp = S + uint32_t(targets.size());
   const uint64_t row = 2ull * K * K;  // bytes per T2 row
-  if (row * Sp > kPairMaxT2 || 2 * (K - 1) > 255) return false;
+  if (row * Sp > kPairMaxT2 || (DGREP_PAIR_U8 && 2 * (K - 1) > 255)) return false;
   const uint64_t t1_off = (kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
   if (end > kPairMaxImage) return false;
   std::vector<uint32_t> id(S), orig(Sp);
@@ -222,7 +222,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   const uint32_t thr_id = S - 1;
   auto premul = [&](uint32_t i) { return uint16_t(kPairT2 + uint64_t(i) * row); };
   img->assign(end, 0);
-  uint8_t* cl = img->data();
+  uint32_t* ua = reinterpret_cast<uint32_t*>(img->data());
+  uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + 1024);
   uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data() + kPairT2);
   uint16_t* t1 = reinterpret_cast<uint16_t*>(img->data() + t1_off);
   for (uint32_t i = 0; i < Sp; ++i) {
@@ -237,7 +238,15 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
       }
     }
   }
-  for (int b = 0; b < 256; ++b) cl[b] = uint8_t(2u * h.byte_class[b]);
+  for (int b = 0; b < 256; ++b) {
+    const uint32_t c = h.byte_class[b];
+    if (DGREP_PAIR_U8) {
+      img->data()[b] = uint8_t(2u * c);  // CL[b]
+    } else {
+      ua[b] = 2u * K * c;
+      ub[b] = 2u * c;
+    }
+  }
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
   pa->t1 = uint32_t(t1_off);
@@ -246,7 +255,7 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   return true;
 }
 
-// The filter stepper's LDS image (StepFilter, scan_dfa.hip): u8 byte classes,
+// The filter stepper's LDS image (StepFilter, scan_dfa.hip): byte classes (kFilterClassBytes),
 // then u16 rows of the DFA's first
 // R - 2 states in breadth-first order from start (start_m at depth 0), as many
 // rows as kFilterImageBytes holds, plus CAND (every transition out of them;
@@ -282,8 +291,10 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
   const uint32_t Sf = next;
   auto to = [&](uint32_t x) { return uint16_t((id[x] == UINT32_MAX ? CAND : id[x]) * K); };
   img->assign((kFilterClassBytes + size_t(Sf) * K * 2 + 15) & ~size_t(15), 0);
-  uint8_t* cls = img->data();
-  for (int b = 0; b < 256; ++b) cls[b] = uint8_t(h.byte_class[b]);
+  for (int b = 0; b < 256; ++b) {
+    if (DGREP_FILTER_CLS32) reinterpret_cast<uint32_t*>(img->data())[b] = h.byte_class[b];
+    else img->data()[b] = h.byte_class[b];
+  }
   uint16_t* rows = reinterpret_cast<uint16_t*>(img->data() + kFilterClassBytes);
   for (uint32_t i = 0; i < keep; ++i) {
     const uint32_t x = order[i];
@@ -505,13 +516,10 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     std::vector<uint32_t> id(S);
     for (uint32_t x = 0; x < S; ++x) id[x] = x;
     std::swap(id[h.start_m], id[top]);
-    // V[b] at b * 8, or (DGREP_SHENG_LP) 32 lane-private copies at b * 256 + 8 * j
-    const size_t stride = kShengImageBytes / 256, copies = stride / 8;
-    t.assign(kShengImageBytes, 0);
+    t.assign(256 * 8, 0);
     for (int b = 0; b < 256; ++b)
       for (uint32_t s = 0; s < S; ++s)
-        for (size_t j = 0; j < copies; ++j)
-          t[size_t(b) * stride + 8 * j + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
+        t[size_t(b) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
     start = id[h.start] * 0x01010101u;
     start_m = top;
   } else {
