@@ -119,33 +119,6 @@ __device__ __forceinline__ uint32_t range_mask(uint64_t w, uint64_t lo, uint64_t
   return m;
 }
 
-// true iff the value bytes [st, st + L) encode as themselves (plain printable
-// ASCII, nothing to escape): aligned 16-byte reads + SWAR tests, no per-byte
-// loads. The common case of text logs; otherwise json_body's byte loop.
-__device__ __forceinline__ bool plain_value(const uint8_t* data, uint64_t n, uint64_t st, uint64_t L) {
-  const uint64_t e = st + L;
-  for (uint64_t q = st & ~uint64_t(15); q < e; q += 16) {
-    if (q + 16 > n) {
-      for (uint64_t i = q > st ? q : st; i < e; ++i) {
-        const uint32_t b = data[i];
-        if (b < 0x20 || b >= 0x80 || b == '"' || b == '\\' || b == '<' || b == '>' || b == '&') return false;
-      }
-      return true;
-    }
-    const uint4 v = *reinterpret_cast<const uint4*>(data + q);
-    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-    uint32_t bad = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint64_t w = q + 4u * uint32_t(k);
-      const uint32_t in = (w >= st && w + 4 <= e) ? 0x80808080u : range_mask(w, st, e);
-      bad |= special_bytes(ws[k]) & in;
-    }
-    if (bad) return false;
-  }
-  return true;
-}
-
 // dst[0:L) = src[0:L) with 4-byte stores after the head: the source is read in
 // aligned dwords and realigned with v_alignbyte (whole-dword reads never pass
 // the source's last dword, which lies inside the 16-B-aligned split).
@@ -175,31 +148,64 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
 // {"Key":" + name + " (line number #" + digits + ")" + ,"Value":" + value + "}\n
 constexpr uint32_t kFixedBytes = 8 + 15 + 2 + 10 + 3;
 
-__device__ inline uint32_t ndigits(uint64_t v) {
-  uint32_t d = 1;
-  while (v >= 10) { v /= 10; ++d; }
-  return d;
+
+// decimal digits of v (most significant first) into d[20]; returns their count.
+// Line numbers below 2^32 (every split under 4 G lines) take the 32-bit path,
+// whose division by 10 is a multiply-high (the 64-bit one is a library loop).
+__device__ __forceinline__ uint32_t digits_of(uint64_t v, uint8_t (&d)[20]) {
+  uint8_t t[20];
+  uint32_t nd = 0;
+  if (v < (1ull << 32)) {
+    uint32_t x = uint32_t(v);
+    do { t[nd++] = uint8_t(x % 10u); x /= 10u; } while (x);
+  } else {
+    do { t[nd++] = uint8_t(v % 10u); v /= 10u; } while (v);
+  }
+  for (uint32_t k = 0; k < nd; ++k) d[k] = t[nd - 1 - k];
+  return nd;
 }
 
+// Per record (one thread each): the key's partition and the encoded line's
+// length ASSUMING a plain value (nothing to escape); encode_values_kernel
+// corrects the length of the rare values that need escaping.
 __global__ __launch_bounds__(kEncThreads) void encode_measure_kernel(EncodeArgs a, uint16_t* part, uint32_t* idx,
                                                                      uint64_t* enc_len) {
   for (uint64_t i = uint64_t(blockIdx.x) * kEncThreads + threadIdx.x; i < a.count;
        i += uint64_t(gridDim.x) * kEncThreads) {
-    const uint64_t ln = a.line_no[i];
-    const uint32_t nd = ndigits(ln);
-    uint64_t p10 = 1;
-    for (uint32_t k = 1; k < nd; ++k) p10 *= 10;
+    uint8_t d[20];
+    const uint32_t nd = digits_of(a.line_no[i], d);
     uint32_t h = a.key_hash0;
-    for (uint64_t v = ln; p10; p10 /= 10) {
-      h = fnv_step(h, uint32_t('0' + v / p10));
-      v %= p10;
-    }
+    for (uint32_t k = 0; k < nd; ++k) h = fnv_step(h, uint32_t('0') + d[k]);
     h = fnv_step(h, uint32_t(')'));
     part[i] = uint16_t((h & 0x7fffffffu) % a.nreduce);
     idx[i] = uint32_t(i);
-    const uint64_t st = a.start[i], L = a.len[i];
-    const uint64_t body = plain_value(a.data, a.n, st, L) ? L : json_body<false>(a.data + st, L, nullptr);
-    enc_len[i] = kFixedBytes + a.fname_json_len + nd + body;
+    enc_len[i] = kFixedBytes + a.fname_json_len + nd + a.len[i];
+  }
+}
+
+// One WAVE per record: the value's bytes are tested 4 per lane (aligned
+// dwords, SWAR) and a ballot decides; a value with anything to escape gets its
+// exact encoded length from json_body (lane 0). Consecutive lanes read
+// consecutive dwords, so a record's value is one coalesced sweep.
+__global__ __launch_bounds__(kEncThreads) void encode_values_kernel(EncodeArgs a, uint64_t* enc_len) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t waves = uint64_t(gridDim.x) * (kEncThreads / 64);
+  for (uint64_t i = uint64_t(blockIdx.x) * (kEncThreads / 64) + (threadIdx.x >> 6); i < a.count; i += waves) {
+    const uint64_t st = a.start[i], e = st + a.len[i];
+    bool bad = false;
+    for (uint64_t w = (st & ~uint64_t(3)) + 4u * lane; w < e; w += 256) {
+      uint32_t x;
+      if (w + 4 <= a.n) {
+        x = *reinterpret_cast<const uint32_t*>(a.data + w);
+      } else {  // the split's last partial dword: no read past n
+        x = 0x20202020u;
+        for (uint32_t k = 0; w + k < a.n; ++k) x = (x & ~(0xffu << (8 * k))) | (uint32_t(a.data[w + k]) << (8 * k));
+      }
+      const uint32_t in = (w >= st && w + 4 <= e) ? 0x80808080u : range_mask(w, st, e);
+      bad = bad || (special_bytes(x) & in) != 0u;
+    }
+    if (__ballot(bad) == 0ull) continue;  // wave-uniform: plain value
+    if (lane == 0) enc_len[i] += json_body<false>(a.data + st, e - st, nullptr) - (e - st);
   }
 }
 
@@ -226,40 +232,134 @@ __device__ inline void put_str(uint8_t*& o, const char* s) {
   while (*s) *o++ = uint8_t(*s++);
 }
 
+// Per-thread writer of one record's line (values that need escaping).
+__device__ void write_line_thread(const EncodeArgs& a, uint64_t i, uint8_t* o, uint64_t enc) {
+  put_str(o, "{\"Key\":\"");
+  for (uint32_t k = 0; k < a.fname_json_len; ++k) *o++ = a.fname_json[k];
+  put_str(o, " (line number #");
+  uint8_t d[20];
+  const uint32_t nd = digits_of(a.line_no[i], d);
+  for (uint32_t k = 0; k < nd; ++k) *o++ = uint8_t('0' + d[k]);
+  put_str(o, ")\",\"Value\":\"");
+  const uint64_t L = a.len[i];
+  if (enc == kFixedBytes + a.fname_json_len + nd + L) {
+    copy_bytes(o, a.data + a.start[i], L);
+    o += L;
+  } else {
+    o += json_body<true>(a.data + a.start[i], L, o);
+  }
+  put_str(o, "\"}\n");
+}
+
+// One WAVE per 64 output lines (sorted order j0 .. j0 + 63). Lane l first
+// fetches line j0 + l's record (coalesced: idx, pos, length, then the record)
+// and writes its line number's digits to the wave's LDS row; then the wave
+// walks the 64 lines, each broadcast from its lane, and lane l builds the
+// line's output dwords (pos >> 2) + l + 64k from its five pieces -- the
+// constant head `{"Key":"<file> (line number #` (LDS), the digits (LDS),
+// `)","Value":"`, the value bytes, `"}\n`. A dword wholly inside the value is
+// one unaligned read of the split (two aligned dwords + v_alignbyte); the
+// first and last dwords of a line, shared with its neighbours, are stored byte
+// by byte. A value that needs escaping is written by its own lane alone
+// (write_line_thread).
+constexpr uint32_t kHeadMax = 2048;
+constexpr int kEncWaves = kEncThreads / 64;
 __global__ __launch_bounds__(kEncThreads) void encode_write_kernel(EncodeArgs a, const uint32_t* idx,
                                                                    const uint64_t* pos, const uint64_t* len_sorted,
                                                                    uint8_t* out, uint64_t out_cap) {
+  __shared__ uint8_t head[kHeadMax];
+  __shared__ uint8_t dig[kEncWaves][64][20];
+  const uint32_t F = a.fname_json_len, A = 8u + F + 15u;  // head bytes (host guarantees A <= kHeadMax)
+  for (uint32_t k = threadIdx.x; k < A; k += kEncThreads)
+    head[k] = k < 8u ? uint8_t("{\"Key\":\""[k]) : k < 8u + F ? a.fname_json[k - 8u] : uint8_t(" (line number #"[k - 8u - F]);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t nwaves = uint64_t(gridDim.x) * kEncWaves;
+  for (uint64_t j0 = (uint64_t(blockIdx.x) * kEncWaves + wv) * 64u; j0 < a.count; j0 += nwaves * 64u) {
+    const uint64_t jm = j0 + lane;
+    uint64_t P = 0, T = 0, st = 0, L = 0, i = 0;
+    uint32_t nd = 0;
+    if (jm < a.count) {
+      i = idx[jm];
+      P = pos[jm];
+      T = len_sorted[jm];
+      st = a.start[i];
+      L = a.len[i];
+      uint8_t d[20];
+      nd = digits_of(a.line_no[i], d);
+      for (uint32_t k = 0; k < nd; ++k) dig[wv][lane][k] = d[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t cnt = uint32_t(min(uint64_t(64), a.count - j0));
+    for (uint32_t r = 0; r < cnt; ++r) {
+      const uint64_t Pr = __shfl(P, int(r), 64), Tr = __shfl(T, int(r), 64);
+      const uint64_t str = __shfl(st, int(r), 64), Lr = __shfl(L, int(r), 64);
+      const uint32_t ndr = uint32_t(__shfl(int(nd), int(r), 64));
+      if (Pr + Tr > out_cap) continue;
+      if (Tr != kFixedBytes + F + ndr + Lr) {  // escaped value: wave-uniform, rare
+        if (lane == r) write_line_thread(a, i, out + P, T);
+        continue;
+      }
+      const uint64_t V0 = uint64_t(A) + ndr + 12u;  // line offset of the first value byte
+      const uint64_t d0 = Pr >> 2, d1 = (Pr + Tr + 3) >> 2;
+      for (uint64_t d = d0 + lane; d < d1; d += 64) {
+        const uint64_t q0 = 4u * d;
+        const int64_t o0 = int64_t(q0) - int64_t(Pr);  // line offset of the dword's byte 0
+        const uint64_t src = str + uint64_t(o0 - int64_t(V0));  // split position of byte 0 if it were value
+        if (o0 >= int64_t(V0) && uint64_t(o0) + 4u <= V0 + Lr && ((src + 3) | 3u) < a.n) {
+          const uint32_t sh = uint32_t(src & 3u);
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(a.data + (src & ~uint64_t(3)));
+          const uint32_t lo = w[0], hi = sh ? w[1] : 0u;
+          *reinterpret_cast<uint32_t*>(out + q0) = __builtin_amdgcn_alignbyte(hi, lo, sh);
+          continue;
+        }
+        uint32_t word = 0, have = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+          const int64_t ob = o0 + int64_t(b);
+          if (ob < 0 || uint64_t(ob) >= Tr) continue;
+          const uint64_t o = uint64_t(ob);
+          uint32_t ch;
+          if (o < A) ch = head[o];
+          else if (o < uint64_t(A) + ndr) ch = uint32_t('0') + dig[wv][r][o - A];
+          else if (o < V0) ch = uint8_t(")\",\"Value\":\""[o - A - ndr]);
+          else if (o < V0 + Lr) ch = a.data[str + (o - V0)];
+          else ch = uint8_t("\"}\n"[o - V0 - Lr]);
+          word |= ch << (8 * b);
+          have |= 1u << b;
+        }
+        if (have == 15u) {
+          *reinterpret_cast<uint32_t*>(out + q0) = word;
+        } else {
+          for (uint32_t b = 0; b < 4; ++b)
+            if (have & (1u << b)) out[q0 + b] = uint8_t(word >> (8 * b));
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the LDS digit row is rewritten next round
+  }
+}
+
+// the per-thread writer for file names whose head does not fit kHeadMax
+__global__ __launch_bounds__(kEncThreads) void encode_write_thread_kernel(EncodeArgs a, const uint32_t* idx,
+                                                                          const uint64_t* pos,
+                                                                          const uint64_t* len_sorted, uint8_t* out,
+                                                                          uint64_t out_cap) {
   for (uint64_t j = uint64_t(blockIdx.x) * kEncThreads + threadIdx.x; j < a.count;
        j += uint64_t(gridDim.x) * kEncThreads) {
     if (pos[j] + len_sorted[j] > out_cap) continue;
-    const uint64_t i = idx[j];
-    uint8_t* o = out + pos[j];
-    put_str(o, "{\"Key\":\"");
-    for (uint32_t k = 0; k < a.fname_json_len; ++k) *o++ = a.fname_json[k];
-    put_str(o, " (line number #");
-    const uint64_t ln = a.line_no[i];
-    const uint32_t nd = ndigits(ln);
-    uint64_t v = ln;
-    for (uint32_t k = nd; k-- > 0;) {
-      o[k] = uint8_t('0' + v % 10);
-      v /= 10;
-    }
-    o += nd;
-    put_str(o, ")\",\"Value\":\"");
-    const uint64_t L = a.len[i];
-    if (len_sorted[j] == kFixedBytes + a.fname_json_len + nd + L) {
-      // the measure pass found nothing to escape: the value is copied as is
-      copy_bytes(o, a.data + a.start[i], L);
-      o += L;
-    } else {
-      o += json_body<true>(a.data + a.start[i], L, o);
-    }
-    put_str(o, "\"}\n");
+    write_line_thread(a, idx[j], out + pos[j], len_sorted[j]);
   }
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 inline int grid_for(uint64_t n) { return int(std::min<uint64_t>((n + kEncThreads - 1) / kEncThreads, 8192)); }
+// one wave per record: 4 records per workgroup, at most 8 resident-sized rounds of the chip
+inline int wave_grid_for(uint64_t n) { return int(std::min<uint64_t>((n + 3) / 4, 16384)); }
+// one wave per 64 records
+inline int wave64_grid_for(uint64_t n) { return int(std::min<uint64_t>((n + 255) / 256, 4096)); }
 }  // namespace
 
 hipError_t encode_partitions(const EncodeArgs& a, void* scratch, size_t* scratch_bytes, uint8_t* out,
@@ -298,6 +398,8 @@ hipError_t encode_partitions(const EncodeArgs& a, void* scratch, size_t* scratch
   if (e != hipSuccess || n == 0) return e;
   hipLaunchKernelGGL(encode_measure_kernel, dim3(grid_for(n)), dim3(kEncThreads), 0, s, a, part_in, idx_in, enc_len);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(encode_values_kernel, dim3(wave_grid_for(n)), dim3(kEncThreads), 0, s, a, enc_len);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   size_t tb = tmp;
   if ((e = hipcub::DeviceRadixSort::SortPairs(t, tb, part_in, part_out, idx_in, idx_out, n, 0, end_bit, s)) !=
       hipSuccess)
@@ -309,8 +411,12 @@ hipError_t encode_partitions(const EncodeArgs& a, void* scratch, size_t* scratch
   hipLaunchKernelGGL(bounds_kernel, dim3(grid_for(n)), dim3(kEncThreads), 0, s, part_out, pos, len_sorted, n,
                      a.nreduce, d_bounds);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(encode_write_kernel, dim3(grid_for(n)), dim3(kEncThreads), 0, s, a, idx_out, pos, len_sorted, out,
-                     out_cap);
+  if (8u + a.fname_json_len + 15u <= kHeadMax)
+    hipLaunchKernelGGL(encode_write_kernel, dim3(wave64_grid_for(n)), dim3(kEncThreads), 0, s, a, idx_out, pos,
+                       len_sorted, out, out_cap);
+  else
+    hipLaunchKernelGGL(encode_write_thread_kernel, dim3(grid_for(n)), dim3(kEncThreads), 0, s, a, idx_out, pos,
+                       len_sorted, out, out_cap);
   return hipGetLastError();
 }
 

@@ -125,6 +125,9 @@ constexpr uint32_t kPairMaxImage = 40960;
 #ifndef DGREP_PAIR_U8
 #define DGREP_PAIR_U8 0
 #endif
+#ifndef DGREP_PAIR_ROWPAD
+#define DGREP_PAIR_ROWPAD 1
+#endif
 constexpr uint32_t kPairT2 = DGREP_PAIR_U8 ? 256 : 2048;  // LDS address of T2 (after the byte tables)
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The

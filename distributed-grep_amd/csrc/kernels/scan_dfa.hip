@@ -124,8 +124,19 @@
 #ifndef DGREP_PAIR_CHUNK
 #define DGREP_PAIR_CHUNK 4096
 #endif
+// deferred events (run_block_defer) for the pair stepper; its per-lane LDS
+// park area (128 B) leaves room for 4 slots per lane (the rest spill to HBM)
+#ifndef DGREP_DEFER
+#define DGREP_DEFER 0
+#endif
+#ifndef DGREP_DEFER_LAZY
+#define DGREP_DEFER_LAZY 1
+#endif
+#ifndef DGREP_DEFER_PAIRREAD
+#define DGREP_DEFER_PAIRREAD 1
+#endif
 #ifndef DGREP_PAIR_SLOTS
-#define DGREP_PAIR_SLOTS 16
+#define DGREP_PAIR_SLOTS (DGREP_DEFER ? 4 : 16)
 #endif
 #ifndef DGREP_PAIR_BLOCK
 #define DGREP_PAIR_BLOCK 128
@@ -470,6 +481,7 @@ struct LaneRun {
   // owned line with it instead of reading this chunk again.
   uint32_t mlo, mhi;
   int32_t p1;
+  int32_t pend;      // deferred path: position of the word holding the last '\n' (-1: resolved)
 };
 
 template <int E, bool DIRECT>
@@ -517,6 +529,9 @@ struct Emitter {
   // 32-bit chunk-relative positions, no length checks.
   __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
     const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
+#ifdef DGREP_ABLATE_EMIT
+    if (DGREP_ABLATE_EMIT) { r.nev += (lw == 0xffffffffu); return; }  // ablation build only (wrong results)
+#endif
     if (DIRECT) {
       const uint64_t o = out_base + r.nev;
       if (o < a->capacity) {
@@ -594,6 +609,10 @@ __device__ __forceinline__ void word_step2(const Step& st, uint32_t M, uint32_t 
 template <class Step>
 __device__ __forceinline__ bool word_any(const Step& st, uint32_t M, uint32_t s0, uint32_t s1, uint32_t s2,
                                          uint32_t s3) {
+#ifdef DGREP_ABLATE_EVENTS
+  // ablation build only (wrong results): no event is ever taken, same DFA
+  if (DGREP_ABLATE_EVENTS) return false;
+#endif
   if constexpr (Step::kKind == kStepSheng8)
     return StepSheng8::any4(s0, s1, s2, s3, M);
   else if constexpr (Step::kKind == kStepPair)
@@ -818,6 +837,127 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   blk_finish(b, s, r);
 }
 
+// Deferred events (Pair stepper). The per-word event branch of run_block is
+// entered whenever ANY of the wave's 64 lanes ends a matching line in that
+// word (C3, 15 % matching lines: about 27 % of all words), and each entry runs
+// its whole emit path for one or two active lanes. Here a block's 32 words are
+// stepped with no branch at all: each word only shifts two bits into per-lane
+// masks -- `evb` (the word ends a matching line) and `hb` (the word holds a
+// '\n') -- and counts its '\n'. The block's raw words are parked in this lane's
+// LDS area, and after the block each lane walks only its OWN event words
+// (about 1.5 iterations per block for the wave instead of ~9 branch entries),
+// re-reading the event word and the previous '\n' word from the park. A word
+// with two or more '\n' breaks the one-'\n'-per-word arithmetic (nls !=
+// popc(hb)); a lane with such a word and an event in the block re-runs the
+// block on the exact per-word path, as does every block past the chunk end.
+// Park layout: 16-B piece i of the block at 16 * (i ^ ((lane >> 1) & 7)),
+// which keeps the ds_write_b128 of all 64 lanes bank-conflict-free.
+template <class Step>
+constexpr bool use_defer() {
+  return DGREP_DEFER && Step::kKind == kStepPair;
+}
+__device__ __forceinline__ uint32_t park_word(const uint8_t* park, uint32_t psw, uint32_t j) {
+  return *reinterpret_cast<const uint32_t*>(park + 16u * ((j >> 2) ^ psw) + 4u * (j & 3u));
+}
+// r.prev_nl of a deferred block whose last '\n' sits in word `r.pend` (block
+// position + 4 * word) of the park: read it before the park is overwritten
+template <int BK>
+__device__ __forceinline__ void defer_resolve(LaneRun& r, const uint8_t* park, uint32_t psw) {
+  // branch-free: the read stays in the block's basic block, its use sinks
+  const uint32_t x = park_word(park, psw, (uint32_t(r.pend) & uint32_t(BK - 1)) >> 2);
+  const int64_t q = int64_t(uint32_t(r.pend) + hi_byte(nl_mask(x)));
+  r.prev_nl = r.pend >= 0 ? q : r.prev_nl;
+  r.pend = -1;
+}
+template <int BK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void run_block_defer(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
+                                                uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit, uint8_t* park,
+                                                uint32_t psw) {
+  defer_resolve<BK>(r, park, psw);
+  if (pos >= C) {  // wave-uniform (every lane of a tile steps the same block offsets)
+    run_block<BK>(st, M, v, pos, C, r, emit);
+    return;
+  }
+  constexpr int NW = BK / 4;
+#pragma unroll
+  for (int i = 0; i < BK / 16; ++i) *reinterpret_cast<uint4*>(park + 16u * (uint32_t(i) ^ psw)) = v[i];
+  uint32_t w[NW];
+#pragma unroll
+  for (int i = 0; i < BK / 16; ++i) {
+    w[4 * i + 0] = v[i].x;
+    w[4 * i + 1] = v[i].y;
+    w[4 * i + 2] = v[i].z;
+    w[4 * i + 3] = v[i].w;
+  }
+  uint32_t s = r.s, evb = 0, hb = 0, nls = 0;
+  typename Step::Pre pre = st.prep(w[0]);
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const typename Step::Pre cur = pre;
+    if (j + 1 < NW) pre = st.prep(w[j + 1 < NW ? j + 1 : 0]);
+    const uint32_t m = nl_mask(w[j]);
+    uint32_t s0, s1, s2, s3;
+    st.apply(cur, s, s0, s1, s2, s3);
+    s = s3;
+    nls += uint32_t(__popc(m));
+    hb = (hb << 1) | uint32_t(m != 0u);
+    evb = (evb << 1) | uint32_t(word_any(st, M, s0, s1, s2, s3));
+  }
+  // word j sits at bit NW-1-j of evb / hb
+  if (evb != 0u && nls != uint32_t(__popc(hb))) {
+    // exact path from the block's start state, over the parked words (the
+    // block's registers are dead by now)
+    uint4 u[BK / 16];
+#pragma unroll
+    for (int i = 0; i < BK / 16; ++i) u[i] = *reinterpret_cast<const uint4*>(park + 16u * (uint32_t(i) ^ psw));
+    run_block<BK>(st, M, u, pos, C, r, emit);
+    return;
+  }
+  const uint32_t p32 = uint32_t(pos);
+  while (evb) {
+    const uint32_t jb = 31u - uint32_t(__clz(evb));  // highest bit = lowest word
+    evb &= ~(1u << jb);
+    const uint32_t j = uint32_t(NW - 1) - jb;
+    const uint32_t hp = jb + 1u < 32u ? hb >> (jb + 1u) : 0u;  // words 0..j-1 (word j-1 at bit 0)
+    if constexpr (DGREP_DEFER_PAIRREAD) {
+      // both park reads issued together (one LDS round trip): the event word
+      // and the word of the previous '\n' (a harmless re-read of word j if none)
+      const uint32_t jp = hp ? j - 1u - uint32_t(__builtin_ctz(hp)) : j;
+      const uint32_t x = park_word(park, psw, j), y = park_word(park, psw, jp);
+      const uint32_t k = uint32_t(__builtin_ctz(nl_mask(x))) >> 3;  // exactly one '\n': the event
+      const uint32_t prev = hp ? p32 + 4u * jp + hi_byte(nl_mask(y)) : uint32_t(r.prev_nl);
+      if (hp || r.seen) emit.inner(r, p32 + 4u * j + k, prev + 1u, r.nl + uint32_t(__popc(hp)), false);
+    } else {
+      const uint32_t m = nl_mask(park_word(park, psw, j));  // exactly one '\n': the event
+      const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
+      uint32_t prev;
+      bool own;
+      if (hp) {
+        const uint32_t jp = j - 1u - uint32_t(__builtin_ctz(hp));
+        prev = p32 + 4u * jp + hi_byte(nl_mask(park_word(park, psw, jp)));
+        own = true;
+      } else {
+        prev = uint32_t(r.prev_nl);
+        own = r.seen;
+      }
+      if (own) emit.inner(r, p32 + 4u * j + k, prev + 1u, r.nl + uint32_t(__popc(hp)), false);
+    }
+  }
+  r.s = s;
+  r.nl += nls;
+  if (hb) {
+    const uint32_t jl = uint32_t(NW - 1) - uint32_t(__builtin_ctz(hb));
+    if constexpr (DGREP_DEFER_LAZY) {
+      // the block's last '\n' (the next line's start) is resolved at the next
+      // block's entry (defer_resolve), where its park read overlaps the stepping
+      r.pend = int32_t(p32 + 4u * jl);
+    } else {
+      r.prev_nl = int64_t(p32 + 4u * jl + hi_byte(nl_mask(park_word(park, psw, jl))));
+    }
+    r.seen = true;
+  }
+}
+
 // Split loads. NT: non-temporal (streaming) loads, so the once-read split does
 // not evict what must stay in L2 (the wide stepper's cold table rows).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -873,15 +1013,29 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
   r.mlo = 0x03020100u;  // identity map
   r.mhi = 0x07060504u;
   r.p1 = -1;
+  r.pend = -1;
 }
 
 // Runs a lane (see file comment) from chunk-relative position pos0 over
 // BK-byte blocks with direct per-lane loads, prefetching the next block while
 // the current one is stepped (two register buffers, ping-pong). Returns the
 // number of '\n' inside the lane's own chunk [cs, cs + C).
-template <int BK, class Step, int E, bool DIRECT>
+template <int BK, bool DEFER = false, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void step_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
+                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit, uint8_t* park,
+                                           uint32_t psw) {
+  if constexpr (DEFER)
+    run_block_defer<BK>(st, M, v, pos, C, r, emit, park, psw);
+  else
+    run_block<BK>(st, M, v, pos, C, r, emit);
+}
+
+// DEFER: blocks inside the chunk go through run_block_defer (park: this lane's
+// BK-byte LDS area, psw its piece swizzle)
+template <int BK, bool DEFER = false, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step& st, uint64_t cs, uint64_t pos0,
-                                                  LaneRun& r, const Emitter<E, DIRECT>& emit, const uint32_t C) {
+                                                  LaneRun& r, const Emitter<E, DIRECT>& emit, const uint32_t C,
+                                                  uint8_t* park = nullptr, uint32_t psw = 0) {
   const uint32_t M = a.start_m;
   const uint64_t avail = cs < a.n ? a.n - cs : 0;
   if (avail <= pos0) {
@@ -899,28 +1053,38 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   for (;;) {
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
-    if (pos + BK > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
+    if (pos + BK > avail) {
+      if constexpr (DEFER) defer_resolve<BK>(r, park, psw);
+      run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);
+      break;
+    }
     load_block<BK, nt_loads<Step>()>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
-    run_block<BK>(st, M, A, pos, uint64_t(C), r, emit);
+    step_block<BK, DEFER>(st, M, A, pos, uint64_t(C), r, emit, park, psw);
     pos += BK;
 
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
-    if (pos + BK > avail) { run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit); break; }
+    if (pos + BK > avail) {
+      if constexpr (DEFER) defer_resolve<BK>(r, park, psw);
+      run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);
+      break;
+    }
     load_block<BK, nt_loads<Step>()>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
-    run_block<BK>(st, M, B, pos, uint64_t(C), r, emit);
+    step_block<BK, DEFER>(st, M, B, pos, uint64_t(C), r, emit, park, psw);
     pos += BK;
   }
+  if constexpr (DEFER) defer_resolve<BK>(r, park, psw);
   if (!snap) nl_chunk = r.nl;
   return nl_chunk;
 }
 
-template <int BK, class Step, int E, bool DIRECT>
+template <int BK, bool DEFER = false, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
-                                             const Emitter<E, DIRECT>& emit, const uint32_t C) {
+                                             const Emitter<E, DIRECT>& emit, const uint32_t C,
+                                             uint8_t* park = nullptr, uint32_t psw = 0) {
   lane_init(a, cs, r);
   if (cs >= a.n) return 0;
-  return run_lane_from<BK>(a, st, cs, 0, r, emit, C);
+  return run_lane_from<BK, DEFER>(a, st, cs, 0, r, emit, C, park, psw);
 }
 
 // Two chunks per lane (csa, csb), both wholly inside the split, stepped in
@@ -1097,6 +1261,9 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   // the same object, hipcc cannot tell a ring write (global_load_lds) from a
   // table read and drains vmcnt before every table lookup
   __shared__ __attribute__((aligned(16))) uint8_t stage[kStaged ? (NT / 64) * DGREP_STAGE_DEPTH * 64 * R : 16];
+  // the park (NT * BK bytes) keeps 3 workgroups per CU only beside tables up to 12 KiB
+  constexpr bool kDefer = use_defer<Step>() && !kStaged && TBL <= 12288;
+  __shared__ __attribute__((aligned(16))) uint8_t park[kDefer ? NT * BK : 16];
   const int tid = int(threadIdx.x);
   for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += NT * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
@@ -1135,6 +1302,8 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
                                          em);
         else
           nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
+      } else if constexpr (kDefer) {
+        nlc[0] = run_lane<BK, true>(a, st, cs[0], r[0], em, C, park + tid * BK, uint32_t(lane >> 1) & 7u);
       } else {
         nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
       }
@@ -1464,6 +1633,7 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
   if (kind == kStepPair) {
     if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
+    if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB): 3 workgroups per CU with the park
     if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
     return op.template run<StepPair, int(kPairMaxImage)>();
   }
@@ -1488,9 +1658,17 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
 // of sending many lanes through the overflow pass (C4 at 16 KiB: 0.8 % of the
 // lanes overflow and the pass costs 8 % of the scan; at 8 KiB 0.07 %).
 constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
-uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c, uint64_t dens_cap) {
+// Per-stepper ceiling: the pair stepper peaks at 16 KiB on C3 (measured on
+// MI355X, nodefer: 8 KiB 4.43 ms, 16 KiB 4.39, 32 KiB 4.71 per 16 GiB): at
+// 32 KiB most of its ~40 records per lane and tile no longer fit the LDS slots
+// and go through the HBM spill area.
+#ifndef DGREP_PAIR_MAX_CHUNK
+#define DGREP_PAIR_MAX_CHUNK 16384
+#endif
+uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c, uint64_t dens_cap,
+                              uint64_t max_c = kShengMaxChunk) {
   uint64_t c = floor_c;
-  while (c * 2 <= kShengMaxChunk && n >= waves * uint64_t(kTileLanes) * c * 2 && (!dens_cap || c * 2 <= dens_cap))
+  while (c * 2 <= max_c && n >= waves * uint64_t(kTileLanes) * c * 2 && (!dens_cap || c * 2 <= dens_cap))
     c *= 2;
   return uint32_t(c);
 }
@@ -1516,7 +1694,8 @@ struct TileOp {
     const uint64_t dens_cap = density > 0 ? uint64_t(double(cap) / (4.0 * density)) : 0;
     if constexpr (adaptive_chunk<S, T>())
       c = force ? uint64_t(force)
-                : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap);
+                : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap,
+                                       S::kKind == kStepPair ? DGREP_PAIR_MAX_CHUNK : kShengMaxChunk);
     *chunk = uint32_t(c);
     *waves_per_block = uint32_t(threads_of<S>() / 64);
     *bytes = uint64_t(kTileLanes) * uint64_t(streams_of<S, T>()) * c;

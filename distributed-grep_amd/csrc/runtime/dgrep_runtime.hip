@@ -204,7 +204,10 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
       if (std::find(targets.begin(), targets.end(), y) == targets.end()) targets.push_back(y);
     }
   const uint32_t Sp = S + uint32_t(targets.size());
-  const uint64_t row = 2ull * K * K;  // bytes per T2 row
+  // bytes per T2 row: 2K^2, padded to an ODD number of dwords so that the
+  // same column of different rows falls in different LDS banks
+  uint64_t row = 2ull * K * K;
+  if (DGREP_PAIR_ROWPAD) row = ((row + 3) & ~3ull) | 4ull;
   if (row * Sp > kPairMaxT2 || (DGREP_PAIR_U8 && 2 * (K - 1) > 255)) return false;
   const uint64_t t1_off = (kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
   if (end > kPairMaxImage) return false;
@@ -234,7 +237,7 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
       t1[size_t(i) * K + c1] = premul(id[a]);
       for (uint32_t c2 = 0; c2 < K; ++c2) {
         const uint32_t y = T(a, c2);
-        t2[(size_t(i) * K + c1) * K + c2] = premul(flagged ? shadow_of[y] : id[y]);
+        t2[size_t(i) * (row / 2) + size_t(c1) * K + c2] = premul(flagged ? shadow_of[y] : id[y]);
       }
     }
   }

@@ -142,3 +142,18 @@ def test_encode_device_capacity_retry(ctx):
     want = expected_partitions(b"error", b"x.log", buf.cpu().numpy().tobytes(), 10)
     assert [raw[x:y] for x, y in zip(b, e)] == want
     assert ctx.last_encode_ms() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("filename", [b"f" * 2100, b"dir/" + b"<&>" * 700, b"a"])
+def test_partitions_head_sizes(ctx, filename):
+    """The wave writer keeps the line head `{"Key":"<file> (line number #` in
+    LDS (2 KiB); longer file names take the per-thread writer. Short and empty
+    lines put line edges at every dword phase of the output."""
+    import dgrep
+
+    lines = [b"error" + b"x" * (k % 9) for k in range(3000)] + [b"error", b"", b"error\xff\"<"]
+    data = b"\n".join(lines) + b"\n" + dgrep.synth_corpus_host(1 << 20, 4, 0)
+    ctx.load(b"error|^$")
+    got = ctx.map_partitions(filename, data, 7)
+    assert got == expected_partitions(b"error|^$", filename, data, 7)

@@ -523,6 +523,35 @@ def test_pair_stepper_dense_overflow(pair_ctx):
         _check(gpu_ctx, pattern, data2)
 
 
+@pytest.mark.parametrize("chunk", [4096, 32768])
+def test_pair_deferred_events_line_shapes(pair_ctx, chunk):
+    """The pair stepper's deferred events (run_block_defer): matching and
+    non-matching lines of every length 1..260 B in a rotating order, so every
+    128-B block position holds an event word, a previous '\\n' in the same
+    word / an earlier word / an earlier block, and blocks with several '\\n' in
+    one word next to events (the exact per-word fallback)."""
+    gpu_ctx = pair_ctx
+    rnd = random.Random(chunk)
+    lines = []
+    for i in range(60000):
+        n = rnd.choice([1, 2, 3, 4, 5, 7, 8, 13, 40, 64, 127, 128, 129, 260]) if i % 3 else rnd.randint(1, 260)
+        body = bytes(rnd.choice(b"abxy _-") for _ in range(n - 1))
+        if rnd.random() < 0.3 and n > 8:
+            k = rnd.randint(0, n - 9)
+            body = body[:k] + b"WARN ab" + body[k + 7:]
+        lines.append(body[: n - 1] + b"\n")
+    data = b"".join(lines)
+    try:
+        gpu_ctx.set_lane_chunk(chunk)
+        for pattern in (b"(WARN|ERROR) [a-z_]+", b"^$|b$", b"WARN ab"):
+            cp = gpu_ctx.load(pattern)
+            _check(gpu_ctx, cp, data)
+            _check(gpu_ctx, cp, data[: len(data) // 2 + 13])
+            assert gpu_ctx.scan_stats()["stepper"] == "pair"
+    finally:
+        gpu_ctx.set_lane_chunk(0)
+
+
 @pytest.mark.parametrize("mode", ["table", "pair", "wide"])
 def test_forced_steppers_agree_on_c3(gpu_ctx, mode):
     """C3's regex through each stepper that can hold it (dgrep_set_stepper)."""

@@ -122,3 +122,20 @@ def test_reduce_rejects_malformed(ctx):
         with pytest.raises(dgrep.DgrepError):
             ctx.reduce(bad)
     assert ctx.reduce(b"") == b""
+
+
+def test_reduce_newline_segments_and_short_lines(ctx):
+    """Newline positions come from per-256-KiB-segment passes: inputs of
+    0.5-3 MiB put lines across segment edges; keys and values of every
+    length 0..9 put line edges at every dword phase of the output; escaped
+    lines sit between plain ones."""
+    rows = []
+    for k in range(60000):
+        key = "f%d (line number #%d)" % (k % 7, k)
+        val = "v" * (k % 10) if k % 13 else "eé<%d>\"" % k
+        rows.append((key if k % 11 else key.replace("f", "g "), val))
+    data = b"".join(json.dumps({"Key": kk, "Value": v}, separators=(",", ":"), ensure_ascii=False).encode() + b"\n"
+                    for kk, v in rows)
+    for cut in (len(data), data.rfind(b"\n", 0, 600000) + 1):
+        got = ctx.reduce(data[:cut])
+        check_reduce(got, data[:cut])
