@@ -282,7 +282,10 @@ def verify_windows(buf, n, line_t, start_t, len_t, pattern, k, win):
             continue
         a, b = a0 + i + 1, a0 + j  # whole lines [a, b), b = a '\n'
         text = chunk[i + 1:j]
-        nl_before = int((buf[:a] == 10).sum().item())
+        # 1 GiB pieces: a whole-prefix compare + sum needs ~9 bytes of HBM per
+        # split byte (a 32 GiB C5 split asked for 205 GiB)
+        step = 1 << 30
+        nl_before = sum(int((buf[o:min(a, o + step)] == 10).sum().item()) for o in range(0, a, step))
         oln, ost, ole = O.grep_map(pattern.encode(), text, threads=min(16, os.cpu_count() or 1))
         sel = (start_t >= a) & (start_t < b)
         gl = line_t[sel].cpu().numpy().astype(np.int64)
