@@ -23,7 +23,7 @@ void set_err(char* err, size_t errlen, const std::string& m) {
 }
 
 int serialize(const dgrep::CompiledDfa& d, void** blob, size_t* blob_len) {
-  size_t n = sizeof(dgrep_blob_header) + d.trans.size() * sizeof(uint32_t);
+  size_t n = sizeof(dgrep_blob_header) + (d.trans.size() + d.nfa.size()) * sizeof(uint32_t);
   auto* p = static_cast<uint8_t*>(malloc(n));
   if (!p) return DGREP_E_NOMEM;
   dgrep_blob_header h;
@@ -35,9 +35,11 @@ int serialize(const dgrep::CompiledDfa& d, void** blob, size_t* blob_len) {
   h.nclasses = d.nclasses;
   h.start = d.start;
   h.start_m = d.start_m;
+  h.nfa_bytes = uint32_t(d.nfa.size() * sizeof(uint32_t));
   memcpy(h.byte_class, d.byte_class, 256);
   memcpy(p, &h, sizeof h);
   memcpy(p + sizeof h, d.trans.data(), d.trans.size() * sizeof(uint32_t));
+  if (!d.nfa.empty()) memcpy(p + sizeof h + d.trans.size() * sizeof(uint32_t), d.nfa.data(), h.nfa_bytes);
   *blob = p;
   *blob_len = n;
   return DGREP_OK;
@@ -84,7 +86,10 @@ extern "C" int dgrep_blob_info_get(const void* blob, size_t n, dgrep_blob_info* 
   memcpy(&h, blob, sizeof h);
   if (h.magic != DGREP_BLOB_MAGIC || h.version != DGREP_BLOB_VERSION) return DGREP_E_INVALID;
   if (h.nstates == 0 || h.nclasses == 0 || h.start >= h.nstates || h.start_m >= h.nstates) return DGREP_E_INVALID;
-  if (n != sizeof h + size_t(h.nstates) * h.nclasses * sizeof(uint32_t)) return DGREP_E_INVALID;
+  if (n != sizeof h + size_t(h.nstates) * h.nclasses * sizeof(uint32_t) + h.nfa_bytes) return DGREP_E_INVALID;
+  // a partial DFA carries its NFA program (header of 8 words at least), nothing else does
+  if (bool(h.flags & DGREP_DFA_PARTIAL) != (h.nfa_bytes != 0) || h.nfa_bytes % 4 || (h.nfa_bytes && h.nfa_bytes < 32))
+    return DGREP_E_INVALID;
   info->flags = h.flags;
   info->nstates = h.nstates;
   info->nclasses = h.nclasses;

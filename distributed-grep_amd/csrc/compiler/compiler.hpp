@@ -15,6 +15,7 @@ struct CompiledDfa {
   uint32_t nstates = 0, nclasses = 0, start = 0, start_m = 0;
   uint8_t byte_class[256] = {0};
   std::vector<uint32_t> trans;  // nstates * nclasses, row-major
+  std::vector<uint32_t> nfa;    // DGREP_DFA_PARTIAL: the NFA program (dgrep_blob.h)
 };
 
 // AST -> minimal line-matching DFA (see dfa_builder.cpp). DGREP_OK or DGREP_E_TOO_LARGE.

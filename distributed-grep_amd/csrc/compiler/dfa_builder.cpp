@@ -23,6 +23,7 @@
 // the decoder trie collapses to a handful of nodes for typical patterns.
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -38,6 +39,8 @@ namespace {
 
 constexpr size_t kMaxNfaStates = 4u << 20;
 constexpr size_t kMaxDfaStates = 1u << 21;
+// states a partial DFA keeps (the filter stepper holds at most 65535 rows)
+constexpr size_t kPartialKeep = 65534;
 
 // ---------------------------------------------------------------- NFA ----
 struct NState {
@@ -325,8 +328,11 @@ class DfaBuilder {
     fffd_ = rc.of(kRuneError);
   }
 
-  // returns false if the state budget is exceeded
-  bool run(CompiledDfa* out);
+  // returns false if the state budget is exceeded; then *partial holds the
+  // first states of the construction with CAND (DGREP_DFA_PARTIAL)
+  bool run(CompiledDfa* out, CompiledDfa* partial, size_t budget);
+  // the NFA program of a partial blob (dgrep_blob.h); false above DGREP_NFA_MAX_POS positions
+  bool nfa_program(std::vector<uint32_t>* prog);
 
  private:
   const NfaBuilder& nfa_;
@@ -364,12 +370,13 @@ class DfaBuilder {
 
   // epsilon closure of Q ∪ {start} at a position whose context is
   // (begin, prev_word, next_word, at_end). Returns true if Match is reached.
-  bool closure(const std::vector<int32_t>& q, bool begin, bool prev_word, bool next_word, bool at_end) {
+  bool closure(const std::vector<int32_t>& q, bool begin, bool prev_word, bool next_word, bool at_end,
+               bool with_start = true) {
     ++gen_;
     clos_.clear();
     stack_.clear();
     for (int32_t s : q) stack_.push_back(s);
-    stack_.push_back(start_);
+    if (with_start) stack_.push_back(start_);
     bool wb = prev_word != next_word;
     while (!stack_.empty()) {
       int32_t x = stack_.back();
@@ -433,7 +440,69 @@ class DfaBuilder {
   }
 };
 
-bool DfaBuilder::run(CompiledDfa* out) {
+// NFA program (layout in dgrep_blob.h): the same step the subset construction
+// memoizes per core (DfaBuilder::step), per position instead of per set.
+bool DfaBuilder::nfa_program(std::vector<uint32_t>* prog) {
+  std::vector<int32_t> pos_of(nfa_.st.size(), -1), pos_state;
+  for (size_t i = 0; i < nfa_.st.size(); ++i)
+    if (nfa_.st[i].kind == NState::Set) {
+      pos_of[i] = int32_t(pos_state.size());
+      pos_state.push_back(int32_t(i));
+    }
+  const uint32_t npos = uint32_t(pos_state.size());
+  if (npos > DGREP_NFA_MAX_POS) return false;
+  const uint32_t nw = std::max<uint32_t>(1, (npos + 31) / 32), nrc = uint32_t(rc_.n),
+                 nnodes = uint32_t(dec_.child.size()), nctx = has_word_ ? 4 : 1;
+  std::vector<uint32_t>& g = *prog;
+  g = {DGREP_NFA_MAGIC, npos, nw, nrc, nnodes, nctx, uint32_t(fffd_), has_word_ ? 1u : 0u};
+  for (const auto& ch : dec_.child)
+    for (int b = 0; b < 256; ++b) g.push_back(uint32_t(ch[size_t(b)]));
+  for (int d : dec_.depth) g.push_back(uint32_t(d));
+  for (uint32_t c = 0; c < nrc; ++c) g.push_back(rc_.word[c] ? 1u : 0u);
+  auto bits = [&](std::vector<uint32_t>& v, size_t at) {  // clos_ -> position bitset at v[at..]
+    for (int32_t x : clos_) v[at + size_t(pos_of[size_t(x)]) / 32] |= 1u << (pos_of[size_t(x)] % 32);
+  };
+  const size_t has_at = g.size();
+  g.resize(has_at + size_t(nrc) * nw, 0);
+  for (uint32_t c = 0; c < nrc; ++c)
+    for (uint32_t p = 0; p < npos; ++p)
+      if (rc_.has(nfa_.st[size_t(pos_state[p])].set, int(c))) g[has_at + size_t(c) * nw + p / 32] |= 1u << (p % 32);
+  auto ctx_pw = [&](uint32_t ctx) { return nctx == 4 && (ctx >> 1); };
+  auto ctx_nw = [&](uint32_t ctx) { return nctx == 4 && (ctx & 1); };
+  const size_t init_at = g.size();
+  g.resize(init_at + 2 * size_t(nctx) * nw + 2 * size_t(nctx), 0);
+  for (uint32_t b = 0; b < 2; ++b)
+    for (uint32_t ctx = 0; ctx < nctx; ++ctx) {
+      const bool m = closure({}, b != 0, ctx_pw(ctx), ctx_nw(ctx), false);
+      if (m) g[init_at + 2 * size_t(nctx) * nw + b * nctx + ctx] = 1;
+      else bits(g, init_at + (size_t(b) * nctx + ctx) * nw);
+    }
+  const size_t cl_at = g.size();
+  g.resize(cl_at + size_t(npos) * nctx * nw + size_t(nctx) * nw, 0);
+  const size_t mx_at = cl_at + size_t(npos) * nctx * nw;
+  for (uint32_t p = 0; p < npos; ++p) {
+    const int32_t to = nfa_.st[size_t(pos_state[p])].out;
+    if (to < 0) continue;
+    for (uint32_t ctx = 0; ctx < nctx; ++ctx) {
+      if (closure({to}, false, ctx_pw(ctx), ctx_nw(ctx), false, false)) g[mx_at + size_t(ctx) * nw + p / 32] |= 1u << (p % 32);
+      else bits(g, cl_at + (size_t(p) * nctx + ctx) * nw);
+    }
+  }
+  const size_t end_at = g.size();
+  g.resize(end_at + 4 + 2 * size_t(nw), 0);
+  for (uint32_t b = 0; b < 2; ++b)
+    for (uint32_t pw = 0; pw < 2; ++pw)
+      g[end_at + b * 2 + pw] = closure({}, b != 0, pw != 0 && has_word_, false, true) ? 1u : 0u;
+  for (uint32_t pw = 0; pw < 2; ++pw)
+    for (uint32_t p = 0; p < npos; ++p) {
+      const int32_t to = nfa_.st[size_t(pos_state[p])].out;
+      if (to >= 0 && closure({to}, false, pw != 0 && has_word_, false, true, false))
+        g[end_at + 4 + size_t(pw) * nw + p / 32] |= 1u << (p % 32);
+    }
+  return true;
+}
+
+bool DfaBuilder::run(CompiledDfa* out, CompiledDfa* partial, size_t budget) {
   // byte classes for construction: bytes that every decoder node treats alike
   std::unordered_map<std::string, int> bsig;
   uint8_t bclass[256];
@@ -485,7 +554,25 @@ bool DfaBuilder::run(CompiledDfa* out) {
   };
 
   for (size_t s = 0; s < states.size(); ++s) {
-    if (states.size() > kMaxDfaStates) return false;
+    if (states.size() > budget && s >= 3) {
+      // Over budget: keep the first states (rows [0, L) are complete, in
+      // breadth-first order) and send every other transition to CAND = L.
+      const uint32_t L = uint32_t(std::min<size_t>(s, kPartialKeep));
+      partial->nstates = L + 1;
+      partial->nclasses = uint32_t(K);
+      partial->start = 0;
+      partial->start_m = 1;
+      partial->flags = DGREP_DFA_PARTIAL;
+      memcpy(partial->byte_class, bclass, 256);
+      partial->trans.assign(size_t(L + 1) * size_t(K), L);
+      for (size_t i = 0; i < L; ++i)
+        for (int k = 0; k < K; ++k) {
+          const uint32_t x = uint32_t(trans[i * size_t(K) + size_t(k)]);
+          partial->trans[i * size_t(K) + size_t(k)] = x < L ? x : L;
+        }
+      partial->trans[size_t(L) * size_t(K) + size_t(nl_class)] = 0;
+      return false;
+    }
     const int dnode = states[s].first, core = states[s].second;
     for (int k = 0; k < K; ++k) {
       const int b = rep[size_t(k)];
@@ -630,7 +717,22 @@ int build_dfa(const Re& re, CompiledDfa* out, std::string* err) {
   Decoder dec;
   dec.build(rc);
   DfaBuilder b(nfa, f.start, rc, dec);
-  if (!b.run(out)) { *err = "DFA exceeds the state budget"; return DGREP_E_TOO_LARGE; }
+  // DGREP_DFA_STATE_BUDGET (tests only) lowers the budget so that the partial
+  // DFA + NFA program path can be checked on small patterns
+  size_t budget = kMaxDfaStates;
+  if (const char* e = getenv("DGREP_DFA_STATE_BUDGET")) {
+    const long v = strtol(e, nullptr, 10);
+    if (v >= 3 && size_t(v) < budget) budget = size_t(v);
+  }
+  CompiledDfa part;
+  if (b.run(out, &part, budget)) return DGREP_OK;
+  // over the DFA budget: the first states as a filter, the NFA program decides
+  // the lines that leave them (DGREP_DFA_PARTIAL)
+  if (part.nstates < 3 || !b.nfa_program(&part.nfa)) {
+    *err = "DFA exceeds the state budget and the NFA has more than 256 rune-set positions";
+    return DGREP_E_TOO_LARGE;
+  }
+  *out = std::move(part);
   return DGREP_OK;
 }
 

@@ -77,6 +77,9 @@ struct VerifyArgs {
   StagedLine* staging;
   uint64_t staging_cap;
   unsigned long long* removed;
+  // DGREP_DFA_PARTIAL blobs: the NFA program (dgrep_blob.h) decides the
+  // candidates instead of `full` (verify_nfa_kernel)
+  const uint32_t* nfa;
 };
 
 // A staged line whose len has this bit set is a filter CANDIDATE (kStepFilter):

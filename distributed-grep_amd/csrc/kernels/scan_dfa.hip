@@ -41,6 +41,7 @@
 #include <algorithm>
 
 #include "scan_common.h"
+#include "../../../include/dgrep_blob.h"
 
 // build-time tuning knobs, per stepper (defaults are the shipped
 // configuration, chosen by tools/variant_bench.sh on MI355X):
@@ -1434,23 +1435,13 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
 // read from HBM (L2-resident: [state][class], u16 entries, or u32 above 65535
 // states). A line is read in aligned 16-byte pieces.
 constexpr uint32_t kVerifyHotBytes = 48 * 1024;
-template <typename E>
-__global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
-  __shared__ uint32_t cls[256];
-  __shared__ __attribute__((aligned(16))) E hot[kVerifyHotBytes / sizeof(E)];
-  cls[threadIdx.x] = v.cls[threadIdx.x];
-  const E* full = static_cast<const E*>(v.full);
-  const uint32_t hot_n = v.hot_entries;
-  for (uint32_t i = threadIdx.x; i < hot_n; i += 256) hot[i] = full[i];
-  __syncthreads();
-  const __attribute__((address_space(1))) E* gfull = (const __attribute__((address_space(1))) E*)v.full;
+
+// The tile loop shared by both verification kernels: line_matches(a, e)
+// decides the candidate [a, e) (grep.go:21 on that line).
+template <class Pred>
+__device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_matches) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t waves = uint64_t(gridDim.x) * 4;
-  const uint32_t K = v.nclasses, cn = cls['\n'];
-  auto next = [&](uint32_t s, uint32_t c) -> uint32_t {
-    const size_t i = size_t(s) * K + c;
-    return i < hot_n ? uint32_t(hot[i]) : uint32_t(gfull[i]);
-  };
   for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
     const TileInfo ti = v.tiles[t];
     if (ti.count == 0) continue;
@@ -1465,22 +1456,7 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
         keep = true;
         if (L.len & kCandidateBit) {
           L.len &= ~kCandidateBit;
-          const uint64_t a = L.start, e = L.start + L.len;
-          uint32_t st = v.start;
-          // the next 16-byte piece is loaded while this one is stepped (the
-          // line's bytes come from HBM: the scan read them long ago)
-          uint4 nxt = *reinterpret_cast<const uint4*>(v.data + (a & ~uint64_t(15)));
-          for (uint64_t q = a & ~uint64_t(15); q < e; q += 16) {
-            const uint4 w = nxt;
-            if (q + 16 < e) nxt = *reinterpret_cast<const uint4*>(v.data + q + 16);
-            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              const uint64_t pos = q + uint64_t(j);
-              if (pos >= a && pos < e) st = next(st, cls[(ws[j >> 2] >> (8 * (j & 3))) & 0xffu]);
-            }
-          }
-          keep = next(st, cn) == v.start_m;
+          keep = line_matches(L.start, L.start + L.len);
         }
       }
       const uint64_t m = __ballot(keep);
@@ -1493,6 +1469,185 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
       atomicAdd(v.removed, (unsigned long long)(ti.count - kept));
     }
   }
+}
+
+// Calls f(byte) for every byte of [a, e), read in aligned 16-byte pieces (the
+// next piece is loaded while this one is stepped; the scan read the line long
+// ago, so its bytes come from HBM). f returns false to stop early.
+template <class F>
+__device__ __forceinline__ void for_line_bytes(const uint8_t* data, uint64_t a, uint64_t e, F&& f) {
+  if (a >= e) return;
+  uint4 nxt = *reinterpret_cast<const uint4*>(data + (a & ~uint64_t(15)));
+  for (uint64_t q = a & ~uint64_t(15); q < e; q += 16) {
+    const uint4 w = nxt;
+    if (q + 16 < e) nxt = *reinterpret_cast<const uint4*>(data + q + 16);
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    bool go = true;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t pos = q + uint64_t(j);
+      if (go && pos >= a && pos < e) go = f((ws[j >> 2] >> (8 * (j & 3))) & 0xffu);
+    }
+    if (!go) return;
+  }
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
+  __shared__ uint32_t cls[256];
+  __shared__ __attribute__((aligned(16))) E hot[kVerifyHotBytes / sizeof(E)];
+  cls[threadIdx.x] = v.cls[threadIdx.x];
+  const E* full = static_cast<const E*>(v.full);
+  const uint32_t hot_n = v.hot_entries;
+  for (uint32_t i = threadIdx.x; i < hot_n; i += 256) hot[i] = full[i];
+  __syncthreads();
+  const __attribute__((address_space(1))) E* gfull = (const __attribute__((address_space(1))) E*)v.full;
+  const uint32_t K = v.nclasses, cn = cls['\n'];
+  auto next = [&](uint32_t s, uint32_t c) -> uint32_t {
+    const size_t i = size_t(s) * K + c;
+    return i < hot_n ? uint32_t(hot[i]) : uint32_t(gfull[i]);
+  };
+  verify_tiles(v, [&](uint64_t a, uint64_t e) {
+    uint32_t st = v.start;
+    for_line_bytes(v.data, a, e, [&](uint32_t b) {
+      st = next(st, cls[b]);
+      return true;
+    });
+    return next(st, cn) == v.start_m;
+  });
+}
+
+// ---- NFA verification (DGREP_DFA_PARTIAL) -----------------------------------
+// A pattern whose DFA exceeds the compiler's budget ships its first DFA states
+// (the filter) and an NFA program (include/dgrep_blob.h): per rune class, a
+// bit-parallel step over at most 256 positions (the NFA's rune-set states),
+// with the UTF-8 decoder trie and the context flags (line start, previous rune
+// a word character) the DFA construction uses. One lane per candidate line;
+// the program is small and stays in L2.
+constexpr uint32_t kNfaMaxWords = DGREP_NFA_MAX_POS / 32;
+
+struct NfaView {
+  const int32_t* child;
+  const uint32_t *depth, *word, *has, *init, *init_m, *cl, *mx, *end_init, *end_x;
+  uint32_t nw, nctx, fffd, has_word;
+};
+
+__device__ __forceinline__ NfaView nfa_view(const uint32_t* g) {
+  NfaView n;
+  const uint32_t nw = g[2], nrc = g[3], nnodes = g[4], nctx = g[5], npos = g[1];
+  n.nw = nw;
+  n.nctx = nctx;
+  n.fffd = g[6];
+  n.has_word = g[7];
+  const uint32_t* p = g + 8;
+  n.child = reinterpret_cast<const int32_t*>(p);
+  p += size_t(nnodes) * 256;
+  n.depth = p;
+  p += nnodes;
+  n.word = p;
+  p += nrc;
+  n.has = p;
+  p += size_t(nrc) * nw;
+  n.init = p;
+  p += 2 * nctx * nw;
+  n.init_m = p;
+  p += 2 * nctx;
+  n.cl = p;
+  p += size_t(npos) * nctx * nw;
+  n.mx = p;
+  p += nctx * nw;
+  n.end_init = p;
+  p += 4;
+  n.end_x = p;
+  return n;
+}
+
+struct NfaRun {
+  uint32_t P[kNfaMaxWords];  // positions consumed by the last rune
+  uint32_t begin, pw, node;  // no rune yet on the line; previous rune is a word char; decoder node
+  bool matched;
+};
+
+// one rune of class c (DfaBuilder::step, per position)
+__device__ __forceinline__ void nfa_rune(const NfaView& g, NfaRun& r, uint32_t c) {
+  const uint32_t nwf = g.word[c];
+  const uint32_t ctx = g.has_word ? r.pw * 2u + nwf : 0u;
+  const uint32_t nw = g.nw;
+  const uint32_t* ini = g.init + (size_t(r.begin) * g.nctx + ctx) * nw;
+  const uint32_t* mx = g.mx + size_t(ctx) * nw;
+  bool m = g.init_m[r.begin * g.nctx + ctx] != 0u;
+  uint32_t S[kNfaMaxWords];
+#pragma unroll
+  for (uint32_t j = 0; j < kNfaMaxWords; ++j) S[j] = j < nw ? ini[j] : 0u;
+#pragma unroll
+  for (uint32_t w = 0; w < kNfaMaxWords; ++w) {
+    uint32_t bits = r.P[w];
+    if (bits & (w < nw ? mx[w] : 0u)) m = true;
+    while (bits) {
+      const uint32_t x = w * 32u + uint32_t(__builtin_ctz(bits));
+      bits &= bits - 1u;
+      const uint32_t* row = g.cl + (size_t(x) * g.nctx + ctx) * nw;
+#pragma unroll
+      for (uint32_t j = 0; j < kNfaMaxWords; ++j)
+        if (j < nw) S[j] |= row[j];
+    }
+  }
+  if (m) {
+    r.matched = true;
+    return;
+  }
+  const uint32_t* hc = g.has + size_t(c) * nw;
+#pragma unroll
+  for (uint32_t j = 0; j < kNfaMaxWords; ++j) r.P[j] = j < nw ? (S[j] & hc[j]) : 0u;
+  r.begin = 0;
+  r.pw = g.has_word ? nwf : 0u;
+}
+
+// one byte through the UTF-8 decoder trie (Go's utf8.DecodeRune: a byte that
+// breaks a sequence flushes its pending bytes as U+FFFD and is decoded afresh)
+__device__ __forceinline__ void nfa_byte(const NfaView& g, NfaRun& r, uint32_t b) {
+  int32_t v = g.child[size_t(r.node) * 256 + b];
+  if (r.node != 0 && v == -1) {
+    for (uint32_t i = 0, d = g.depth[r.node]; i < d && !r.matched; ++i) nfa_rune(g, r, g.fffd);
+    r.node = 0;
+    if (r.matched) return;
+    v = g.child[b];
+  }
+  if (v <= -2) {
+    r.node = 0;
+    nfa_rune(g, r, uint32_t(-2 - v));
+  } else if (v == -1) {
+    nfa_rune(g, r, g.fffd);
+  } else {
+    r.node = uint32_t(v);
+  }
+}
+
+__device__ __forceinline__ bool nfa_line_matches(const NfaView& g, const uint8_t* data, uint64_t a, uint64_t e) {
+  NfaRun r;
+#pragma unroll
+  for (uint32_t j = 0; j < kNfaMaxWords; ++j) r.P[j] = 0;
+  r.begin = 1;
+  r.pw = 0;
+  r.node = 0;
+  r.matched = false;
+  for_line_bytes(data, a, e, [&](uint32_t b) {
+    nfa_byte(g, r, b);
+    return !r.matched;
+  });
+  for (uint32_t i = 0, d = g.depth[r.node]; i < d && !r.matched; ++i) nfa_rune(g, r, g.fffd);
+  if (r.matched) return true;
+  bool m = g.end_init[r.begin * 2u + r.pw] != 0u;
+  const uint32_t* ex = g.end_x + size_t(r.pw) * g.nw;
+#pragma unroll
+  for (uint32_t w = 0; w < kNfaMaxWords; ++w)
+    if (w < g.nw && (r.P[w] & ex[w])) m = true;
+  return m;
+}
+
+__global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
+  const NfaView g = nfa_view(v.nfa);
+  verify_tiles(v, [&](uint64_t a, uint64_t e) { return nfa_line_matches(g, v.data, a, e); });
 }
 
 // ---- ordering passes ------------------------------------------------------
@@ -1769,7 +1924,9 @@ hipError_t verify_candidates(const VerifyArgs& v, hipStream_t stream) {
   uint64_t grid = (v.ntiles + 3) / 4;
   if (grid > 16384) grid = 16384;
   if (grid == 0) return hipSuccess;
-  if (v.full_u32)
+  if (v.nfa)
+    hipLaunchKernelGGL(verify_nfa_kernel, dim3(grid), dim3(256), 0, stream, v);
+  else if (v.full_u32)
     hipLaunchKernelGGL(verify_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, v);
   else
     hipLaunchKernelGGL(verify_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, v);

@@ -91,6 +91,7 @@ struct dgrep_ctx {
   uint8_t* d_cls = nullptr;    // [256]
   uint32_t blob_start = 0, blob_start_m = 0;  // start / start_m in d_full's (breadth-first) ids
   uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
+  uint32_t* d_nfa = nullptr;                   // DGREP_DFA_PARTIAL: the NFA program (verify_nfa_kernel)
   int blocks_per_cu = 1;
 
   // per-scan scratch (grown on demand, reused)
@@ -265,8 +266,10 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
 // '\n' -> CAND_END) and CAND_END (start's row). Ids: kept states other than
 // start_m, CAND, start_m, CAND_END; entries premultiplied by K. Returns false
 // if not even start, start_m and their successors fit.
+// `excluded`: a partial blob's CAND state (never kept, so every transition
+// into it is a filter CAND too).
 bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint32_t row_cap, std::vector<uint8_t>* img,
-                        uint32_t* start, uint32_t* start_m, uint32_t* cand_end) {
+                        uint32_t* start, uint32_t* start_m, uint32_t* cand_end, uint32_t excluded = UINT32_MAX) {
   const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
   const uint32_t cn = h.byte_class[uint8_t('\n')];
   // rows that fit (row_cap: dgrep_set_stepper's test knob)
@@ -275,19 +278,20 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
   std::vector<uint32_t> order;
   std::vector<uint8_t> seen(S, 0);
   auto visit = [&](uint32_t x) {
-    if (!seen[x]) { seen[x] = 1; order.push_back(x); }
+    if (!seen[x] && x != excluded) { seen[x] = 1; order.push_back(x); }
   };
   visit(h.start);
   visit(M);
   for (size_t q = 0; q < order.size(); ++q)
     for (uint32_t k = 0; k < K; ++k) visit(trans[size_t(order[q]) * K + k]);
-  const uint32_t keep = std::min<uint32_t>(uint32_t(order.size()), S <= R ? S : R - 2);
+  const bool part = excluded != UINT32_MAX;
+  const uint32_t keep = std::min<uint32_t>(uint32_t(order.size()), S <= R && !part ? S : R - 2);
   if (keep < 2) return false;
   std::vector<uint32_t> id(S, UINT32_MAX);
   uint32_t next = 0;
   for (uint32_t i = 0; i < keep; ++i)
     if (order[i] != M) id[order[i]] = next++;
-  const bool exact = keep == S;  // the whole DFA fits: no candidates
+  const bool exact = keep == S && !part;  // the whole DFA fits: no candidates
   const uint32_t CAND = exact ? UINT32_MAX : next++;
   id[M] = next++;
   const uint32_t CEND = exact ? UINT32_MAX : next++;
@@ -347,7 +351,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_cls, c->d_spill, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -414,9 +418,16 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   std::vector<uint16_t> wide;
   uint32_t start = h.start, start_m = h.start_m;
   const int force = c->force_stepper;
+  // a partial DFA (DGREP_DFA_PARTIAL) runs only as a filter: its last state is
+  // CAND, and the NFA program after `trans` verifies the lines that reach it
+  const bool partial = (h.flags & DGREP_DFA_PARTIAL) != 0;
+  if (partial && force != 0 && force != 4) {
+    c->err = "dgrep_load_dfa: a partial DFA (over the compiler's state budget) runs on the filter stepper only";
+    return DGREP_E_UNSUPPORTED;
+  }
   std::vector<uint8_t> pair_img;
   uint32_t pair_start = 0, pair_m = 0;
-  const bool pair_ok = (force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3
+  const bool pair_ok = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3)
                            ? build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args)
                            : false;
   if (force == 3 && !pair_ok) {
@@ -425,9 +436,10 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   }
   std::vector<uint8_t> filter_img;
   uint32_t f_start = 0, f_m = 0, f_cend = UINT32_MAX;
-  const bool filter_ok = !pair_ok && ((force == 0 && h.nstates > 256) || force == 4) &&
-                         build_filter_image(h, trans, c->wide_hot_rows_cap, &filter_img, &f_start, &f_m, &f_cend);
-  if (force == 4 && !filter_ok) {
+  const bool filter_ok = !pair_ok && ((force == 0 && (h.nstates > 256 || partial)) || force == 4) &&
+                         build_filter_image(h, trans, c->wide_hot_rows_cap, &filter_img, &f_start, &f_m, &f_cend,
+                                            partial ? h.nstates - 1 : UINT32_MAX);
+  if ((force == 4 || partial) && !filter_ok) {
     c->err = "dgrep_load_dfa: the filter stepper cannot hold this DFA's first states";
     return DGREP_E_UNSUPPORTED;
   }
@@ -444,6 +456,23 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     t.swap(filter_img);
     start = f_start;
     start_m = f_m;
+  }
+  c->loaded = false;  // the previous pattern's verification tables go now
+  if (c->d_nfa) HIPCHK(hipFree(c->d_nfa));
+  c->d_nfa = nullptr;
+  if (c->d_full) HIPCHK(hipFree(c->d_full));
+  c->d_full = nullptr;
+  if (pair_ok) {
+    // image built above
+  } else if (filter_ok && partial) {
+    const uint32_t* prog = trans + size_t(h.nstates) * h.nclasses;
+    if (h.nfa_bytes < 32 || prog[0] != DGREP_NFA_MAGIC || prog[1] > DGREP_NFA_MAX_POS) {
+      c->err = "dgrep_load_dfa: malformed NFA program";
+      return DGREP_E_INVALID;
+    }
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_nfa), h.nfa_bytes));
+    HIPCHK(hipMemcpy(c->d_nfa, prog, h.nfa_bytes, hipMemcpyHostToDevice));
+  } else if (filter_ok) {
     // the whole DFA for verify_kernel, renumbered breadth-first from start
     // (start, start_m, then BFS) so its hot rows lead; u16 entries while the
     // ids fit, u32 above 65535 states (up to the compiler's budget)
@@ -460,8 +489,6 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     for (uint32_t x = 0; x < S; ++x) visit(x);
     const size_t ne = size_t(S) * K;
     c->full_u32 = S > 65535;
-    if (c->d_full) HIPCHK(hipFree(c->d_full));
-    c->d_full = nullptr;
     const size_t esz = c->full_u32 ? 4 : 2;
     std::vector<uint8_t> full(ne * esz);
     for (uint32_t n = 0; n < S; ++n)
@@ -704,6 +731,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.staging = c->d_staging;
     v.staging_cap = c->staging_cap;
     v.removed = c->d_counters + 3;  // zeroed before the scan
+    v.nfa = c->d_nfa;
     HIPCHK(hipEventRecord(c->ev4, c->stream));
     HIPCHK(verify_candidates(v, c->stream));
     HIPCHK(hipEventRecord(c->ev5, c->stream));

@@ -45,6 +45,7 @@ DGREP_E_NO_DFA = 6
 DFA_GO_SYNTAX_ERROR = 1
 DFA_MATCH_NONE = 2
 DFA_MATCH_ALL = 4
+DFA_PARTIAL = 8
 
 # Symbols declared in include/dgrep.h (tests check the library exports all).
 EXPORTS = (
@@ -201,13 +202,25 @@ class CompiledPattern:
         self.message = msg
 
     @property
+    def partial(self) -> bool:
+        """DFA over the state budget: first states + CAND, lines that reach CAND
+        are decided by the blob's NFA program (dgrep_blob.h)."""
+        return bool(self.flags & DFA_PARTIAL)
+
+    def nfa_program(self) -> np.ndarray:
+        """The NFA program (u32 words) of a partial blob -- for tests."""
+        ne = self.nstates * self.nclasses
+        return np.frombuffer(self.blob[288 + 4 * ne:], dtype=np.uint32)
+
+    @property
     def go_syntax_error(self) -> bool:
         return bool(self.flags & DFA_GO_SYNTAX_ERROR)
 
     def tables(self) -> Tuple[np.ndarray, np.ndarray]:
         """(byte_class[256] u8, trans[nstates, nclasses] u32) — for tests/inspection."""
         bc = np.frombuffer(self.blob[32:288], dtype=np.uint8)
-        tr = np.frombuffer(self.blob[288:], dtype=np.uint32).reshape(self.nstates, self.nclasses)
+        ne = self.nstates * self.nclasses
+        tr = np.frombuffer(self.blob[288:288 + 4 * ne], dtype=np.uint32).reshape(self.nstates, self.nclasses)
         return bc, tr
 
 

@@ -51,6 +51,7 @@ enum {
   DGREP_DFA_GO_SYNTAX_ERROR = 1u << 0, /* Go's regexp.Compile rejects the pattern: no line matches (grep.go:21 drops err) */
   DGREP_DFA_MATCH_NONE = 1u << 1,      /* no line can match */
   DGREP_DFA_MATCH_ALL = 1u << 2,       /* every line matches (e.g. the shipped pattern "" at grep.go:11) */
+  DGREP_DFA_PARTIAL = 1u << 3,         /* DFA beyond the state budget: first states + CAND + NFA program (dgrep_blob.h) */
 };
 
 typedef struct dgrep_ctx dgrep_ctx;

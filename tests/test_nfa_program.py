@@ -1,0 +1,82 @@
+"""Patterns whose DFA exceeds the compiler's state budget (DGREP_DFA_PARTIAL,
+include/dgrep_blob.h): the blob keeps the first DFA states as a filter and an
+NFA program decides the lines that leave them. On the CPU, both halves are
+interpreted by tests/nfa_runner.py and must reproduce the oracle's Map output
+(grep.go:17-29) bit-exactly. DGREP_DFA_STATE_BUDGET (a test knob read by the
+compiler) forces the partial form on small patterns, so the NFA program is
+checked on the same random patterns as the DFA (test_compiler.py)."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import dgrep
+import oracle_lib as O
+from nfa_runner import NfaProgram, nfa_only, run_partial
+from test_compiler import ALPHA, _rand_pattern
+
+
+def _eq(got, want, what):
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g.astype(np.int64), w.astype(np.int64), err_msg=str(what))
+
+
+@pytest.mark.parametrize("budget", ["3", "12"])
+def test_partial_program_vs_oracle_random(monkeypatch, budget):
+    monkeypatch.setenv("DGREP_DFA_STATE_BUDGET", budget)
+    rnd = random.Random(1000 + int(budget))
+    checked = 0
+    for _ in range(300):
+        pat = _rand_pattern(rnd).encode()
+        if O.compile_status(pat) != O.ORC_OK:
+            continue
+        try:
+            cp = dgrep.CompiledPattern(pat)
+        except dgrep.UnsupportedPattern:
+            continue
+        if not cp.partial:
+            continue  # the whole DFA fits even the lowered budget
+        data = b"".join(rnd.choice(ALPHA) for _ in range(rnd.randint(0, 240)))
+        want = O.grep_map(pat, data)
+        _eq(run_partial(cp, data), want, (pat, data))
+        _eq(nfa_only(cp, data), want, (pat, data))
+        checked += 1
+    assert checked > 150, checked
+
+
+KNOWN = [
+    # pattern, lines (no '\n'); the DFA of each exceeds 2**21 states
+    (b"[ab]*a[ab]{21}", [b"", b"a" * 22, b"b" * 40, b"a" + b"b" * 21, b"a" + b"b" * 20, b"xa" + b"ab" * 11,
+                         b"ab" * 30 + b"c", b"\xffa" + b"b" * 21]),
+    (b"a.{20}$", [b"a" * 21, b"a" * 20, b"xa" + "é".encode() * 20, b"a" + b"\xff" * 20, b"a" + b"\xe2\x82" * 10,
+                  b"za" + "€".encode() * 19 + b"q", b"a" + "€".encode() * 21]),
+]
+
+
+@pytest.mark.parametrize("pattern,lines", KNOWN)
+def test_budget_exceeding_patterns_compile_partial(pattern, lines):
+    cp = dgrep.CompiledPattern(pattern)
+    assert cp.partial and cp.nstates == 65535, (cp.flags, cp.nstates)
+    prog = NfaProgram(cp.nfa_program())
+    assert prog.npos <= 256
+    data = b"\n".join(lines)
+    _eq(run_partial(cp, data), O.grep_map(pattern, data), pattern)
+    for line in lines:
+        assert prog.match(line) == bool(O.Regexp(pattern).match(line)), (pattern, line)
+
+
+def test_blob_info_checks_the_program():
+    cp = dgrep.CompiledPattern(b"[ab]*a[ab]{21}")
+    L = dgrep.lib()
+    info = dgrep._BlobInfo()
+    assert L.dgrep_blob_info_get(cp.blob, len(cp.blob), ctypes.byref(info)) == dgrep.DGREP_OK
+    assert info.flags & dgrep.DFA_PARTIAL
+    # the flag without the program, and the program without the flag, are malformed
+    ne = cp.nstates * cp.nclasses
+    cut = bytearray(cp.blob[:288 + 4 * ne])
+    cut[28:32] = (0).to_bytes(4, "little")
+    assert L.dgrep_blob_info_get(bytes(cut), len(cut), ctypes.byref(info)) == dgrep.DGREP_E_INVALID
+    noflag = bytearray(cp.blob)
+    noflag[8:12] = (0).to_bytes(4, "little")
+    assert L.dgrep_blob_info_get(bytes(noflag), len(noflag), ctypes.byref(info)) == dgrep.DGREP_E_INVALID
