@@ -132,6 +132,27 @@ constexpr uint32_t kPairMaxImage = 40960;
 #define DGREP_PAIR_ROWPAD 1
 #endif
 constexpr uint32_t kPairT2 = DGREP_PAIR_U8 ? 256 : 2048;  // LDS address of T2 (after the byte tables)
+// DGREP_PAIR_SWZ: UA/UB entry of byte b at index swz(b) = b ^ ((b >> 1) & 0x30)
+// (a bijection). Entry i sits in LDS bank i % 64, so unswizzled the digits
+// 0x30-0x39 share banks with 'p'-'y', '-' ':' '.' with 'm' 'z' 'n'...; swizzled,
+// a wave64 class read over log text costs 1.33 bank cycles instead of 1.97
+// (CPU simulation over the C3 corpus, every swizzle of this form searched).
+// OFF: measured slower on MI355X (C3 kernel 4,030 -> 3,860 GB/s, C2 with
+// DGREP_SHENG_SWZ 5,380 -> 4,820): the two VALU per word the swizzle costs
+// outweigh the bank cycles it saves -- these steppers are VALU-issue-bound.
+#ifndef DGREP_PAIR_SWZ
+#define DGREP_PAIR_SWZ 0
+#endif
+// DGREP_SHENG_SWZ: the same for Sheng8's V[b] (8 bytes: banks 2i, 2i+1 of
+// entry i), swz(b) = b ^ ((b >> 2) & 0x0a): 2.13 bank cycles per read instead
+// of 2.39 on the C2 corpus (simulated)
+#ifndef DGREP_SHENG_SWZ
+#define DGREP_SHENG_SWZ 0
+#endif
+__host__ __device__ constexpr uint32_t sheng_swz(uint32_t b) { return DGREP_SHENG_SWZ ? b ^ ((b >> 2) & 0x0au) : b; }
+__host__ __device__ constexpr uint32_t pair_swz(uint32_t b) {
+  return (DGREP_PAIR_SWZ && !DGREP_PAIR_U8) ? b ^ ((b >> 1) & 0x30u) : b;
+}
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
 // runtime renumbers states hottest-first (start, start_m, then BFS order from

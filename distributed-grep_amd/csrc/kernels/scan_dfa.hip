@@ -219,6 +219,7 @@ struct StepSheng8 {
     uint2 m0, m1, m2, m3;
   };
   __device__ __forceinline__ Pre prep(uint32_t x) const {
+    if constexpr (DGREP_SHENG_SWZ) x ^= (x >> 2) & 0x0a0a0a0au;  // sheng_swz of every byte
     return Pre{V[x & 0xffu], V[(x >> 8) & 0xffu], V[(x >> 16) & 0xffu], V[x >> 24]};
   }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
@@ -228,7 +229,7 @@ struct StepSheng8 {
     s2 = sel(p.m2, s1);
     s3 = sel(p.m3, s2);
   }
-  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[b], s); }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[sheng_swz(b)], s); }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return (s & 0xffu) == M; }
   // states are replicated bytes and start_m is the highest state (host
   // renumbering): one max over the word's four states replaces four compares
@@ -312,20 +313,23 @@ struct StepPair {
   struct Pre {
     uint32_t a0, b1, a2, b3;
   };
-  __device__ __forceinline__ uint32_t ua(uint32_t b) const {
+  // raw: b is already swizzled (pair_swz)
+  __device__ __forceinline__ uint32_t ua_raw(uint32_t b) const {
     return *reinterpret_cast<const uint32_t*>(lds + 4u * b);
   }
-  __device__ __forceinline__ uint32_t ub(uint32_t b) const {
+  __device__ __forceinline__ uint32_t ub_raw(uint32_t b) const {
     if constexpr (DGREP_PAIR_U8) return lds[b];  // CL[b] = 2 * class(b)
     return *reinterpret_cast<const uint32_t*>(lds + 1024u + 4u * b);
   }
+  __device__ __forceinline__ uint32_t ub(uint32_t b) const { return ub_raw(pair_swz(b)); }
   __device__ __forceinline__ Pre prep(uint32_t x) const {
     if constexpr (DGREP_PAIR_U8) {
       // a0 = 2K*c0 + 2*c1, a2 = 2K*c2 + 2*c3 (b1 = b3 = 0)
       const uint32_t c0 = lds[x & 0xffu], c1 = lds[(x >> 8) & 0xffu], c2 = lds[(x >> 16) & 0xffu], c3 = lds[x >> 24];
       return Pre{__umul24(c0, K) + c1, 0u, __umul24(c2, K) + c3, 0u};
     }
-    return Pre{ua(x & 0xffu), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu), ub(x >> 24)};
+    if constexpr (DGREP_PAIR_SWZ) x ^= (x >> 1) & 0x30303030u;  // pair_swz of every byte (one v_bitop3)
+    return Pre{ua_raw(x & 0xffu), ub_raw((x >> 8) & 0xffu), ua_raw((x >> 16) & 0xffu), ub_raw(x >> 24)};
   }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
     return *reinterpret_cast<const uint16_t*>(lds + off);

@@ -247,8 +247,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
     if (DGREP_PAIR_U8) {
       img->data()[b] = uint8_t(2u * c);  // CL[b]
     } else {
-      ua[b] = 2u * K * c;
-      ub[b] = 2u * c;
+      ua[pair_swz(uint32_t(b))] = 2u * K * c;
+      ub[pair_swz(uint32_t(b))] = 2u * c;
     }
   }
   *start = premul(id[h.start]);
@@ -549,7 +549,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     t.assign(256 * 8, 0);
     for (int b = 0; b < 256; ++b)
       for (uint32_t s = 0; s < S; ++s)
-        t[size_t(b) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
+        t[size_t(sheng_swz(uint32_t(b))) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
     start = id[h.start] * 0x01010101u;
     start_m = top;
   } else {
