@@ -162,11 +162,36 @@
 namespace dgrep {
 
 
+// DGREP_NL_ASM: the last op of nl_mask and the '\n' count as inline asm, so
+// the compiler neither re-derives "m != 0" from the mask's inputs (it
+// canonicalised that test into v_bitop3 + v_cmp instead of one v_cmp on m) nor
+// splits popcount + sum into v_bcnt + v_add (v_bcnt_u32_b32 accumulates):
+// two VALU fewer per word on the per-word steppers, which are VALU-issue-bound.
+#ifndef DGREP_NL_ASM
+#define DGREP_NL_ASM 1
+#endif
 __device__ __forceinline__ uint32_t nl_mask(uint32_t w) {
   // exact per-byte zero test of w ^ '\n\n\n\n': bit 7 of byte k set iff byte k == '\n'
   uint32_t x = w ^ 0x0a0a0a0au;
+  if constexpr (DGREP_NL_ASM) {
+    const uint32_t t = (x & 0x7f7f7f7fu) + 0x7f7f7f7fu;
+    uint32_t m;
+    // m = ~(t | w) & 0x80808080 (bit 7 of w equals bit 7 of x); truth table
+    // index = (S0 << 2) | (S1 << 1) | S2: true only at S0 = S1 = 0, S2 = 1
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:2" : "=v"(m) : "v"(t), "v"(w), "s"(0x80808080u));
+    return m;
+  }
   uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
   return ~t & 0x80808080u;
+}
+// acc + popcount(m) in one v_bcnt_u32_b32
+__device__ __forceinline__ uint32_t add_popc(uint32_t acc, uint32_t m) {
+  if constexpr (DGREP_NL_ASM) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(m), "v"(acc));
+    return r;
+  }
+  return acc + uint32_t(__popc(m));
 }
 __device__ __forceinline__ uint32_t hi_byte(uint32_t m) { return (31u - __clz(m)) >> 3; }
 
@@ -673,7 +698,7 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
 // newline bookkeeping of word J
 template <int J>
 __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
-  b.nlrun += uint32_t(__popc(m));
+  b.nlrun = add_popc(b.nlrun, m);
   if (m) { b.lastm = m; b.lastj = J; }
 }
 
@@ -904,7 +929,7 @@ __device__ __forceinline__ void run_block_defer(const Step& st, uint32_t M, cons
     uint32_t s0, s1, s2, s3;
     st.apply(cur, s, s0, s1, s2, s3);
     s = s3;
-    nls += uint32_t(__popc(m));
+    nls = add_popc(nls, m);
     hb = (hb << 1) | uint32_t(m != 0u);
     evb = (evb << 1) | uint32_t(word_any(st, M, s0, s1, s2, s3));
   }
