@@ -162,6 +162,14 @@
 namespace dgrep {
 
 
+// DGREP_FLAT_EMIT: the event fast path of the one-stream slot steppers writes
+// its record branch-free -- to LDS slot min(nev, E), slot E being a per-lane
+// dummy, and bumps nev only if the lane owns the line -- instead of nesting
+// exec-mask regions for ownership and slot-vs-spill (the spill write stays a
+// branch, almost always skipped by the whole wave)
+#ifndef DGREP_FLAT_EMIT
+#define DGREP_FLAT_EMIT 1
+#endif
 // DGREP_NL_ASM: the last op of nl_mask and the '\n' count as inline asm, so
 // the compiler neither re-derives "m != 0" from the mask's inputs (it
 // canonicalised that test into v_bitop3 + v_cmp instead of one v_cmp on m) nor
@@ -557,6 +565,18 @@ struct Emitter {
   }
   // The same for a line wholly inside the lane's chunk (start < q < C <= 32 KiB):
   // 32-bit chunk-relative positions, no length checks.
+  // inner() for the slot mode with a dummy slot E (DGREP_FLAT_EMIT): own = the
+  // lane owns the line. A write for a line it does not own lands in a slot (or
+  // spill entry) no record has claimed yet, so it is never read.
+  __device__ __forceinline__ void inner_flat(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand,
+                                             bool own) const {
+    const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
+    const uint32_t w0 = start | (rel << 16);
+    const uint32_t i = min(r.nev, uint32_t(E));
+    *reinterpret_cast<uint2*>(slots + 2u * i) = make_uint2(w0, lw);
+    if (r.nev >= uint32_t(E) && r.nev - uint32_t(E) < spill_cap) spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
+    r.nev += own ? 1u : 0u;
+  }
   __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
     const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
 #ifdef DGREP_ABLATE_EMIT
@@ -593,6 +613,13 @@ struct Blk {
   uint32_t lastm;   // newline mask of the last word with a '\n' (0: none yet)
   int lastj;        // its index
 };
+
+// the steppers whose lanes carry the dummy slot (slot_stride): one stream per lane
+template <class Step, bool DIRECT>
+constexpr bool flat_emit() {
+  // (not Filter: its 1024 threads x 8 B dummy would not fit beside its 124 KiB image)
+  return DGREP_FLAT_EMIT && !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair);
+}
 
 // Everything a word step does after its four DFA steps s0..s3 (newline mask
 // m): matching-line events, the first-piece map (TRACK), newline bookkeeping.
@@ -669,7 +696,11 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
     const uint32_t lastpos = uint32_t(b.pos) + 4u * uint32_t(b.lastj) + hi_byte(b.lastm | 1u);
     const uint32_t prev = b.lastm ? lastpos : uint32_t(r.prev_nl);
     const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
-    if (r.seen | (b.lastm != 0)) emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk));
+    if constexpr (flat_emit<Step, DIRECT>())
+      emit.inner_flat(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk),
+                      r.seen | (b.lastm != 0));
+    else if (r.seen | (b.lastm != 0))
+      emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk));
     return;
   }
   const uint64_t q0 = b.pos + 4u * J;
@@ -1286,7 +1317,10 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   constexpr bool kStaged = use_staging<Step, TBL>();
   const uint32_t C = lane_chunk<Step, TBL>(a);
   constexpr int R = DGREP_STAGE_ROUND;
-  __shared__ ScanSmem<TBL, E * streams_of<Step, TBL>(), NT> sm;
+  // per-lane slot stride: E slots per stream, plus the dummy of flat_emit
+  constexpr int ES = E * streams_of<Step, TBL>() + (flat_emit<Step, false>() ? 1 : 0);
+  static_assert(!flat_emit<Step, false>() || streams_of<Step, TBL>() == 1, "dummy slot: one stream per lane");
+  __shared__ ScanSmem<TBL, ES, NT> sm;
   // the staging rings are a __shared__ object of their own: with the table in
   // the same object, hipcc cannot tell a ring write (global_load_lds) from a
   // table read and drains vmcnt before every table lookup
@@ -1301,7 +1335,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
 
   const Step st = make_step<Step>(sm.tbl, a);
   constexpr int S = streams_of<Step, TBL>();  // chunks per lane: chunk k of a tile is k * 64 + lane
-  uint32_t* slots = sm.slots + tid * S * E * 2;
+  uint32_t* slots = sm.slots + tid * ES * 2;
   const int lane = tid & 63;
   const uint64_t waves = uint64_t(gridDim.x) * (NT / 64);
   const uint64_t kTile = uint64_t(kTileLanes) * uint64_t(S) * uint64_t(C);
