@@ -170,6 +170,9 @@ namespace dgrep {
 #ifndef DGREP_FLAT_EMIT
 #define DGREP_FLAT_EMIT 1
 #endif
+#ifndef DGREP_PAIR_SDWA0
+#define DGREP_PAIR_SDWA0 1
+#endif
 // DGREP_NL_ASM: the last op of nl_mask and the '\n' count as inline asm, so
 // the compiler neither re-derives "m != 0" from the mask's inputs (it
 // canonicalised that test into v_bitop3 + v_cmp instead of one v_cmp on m) nor
@@ -362,6 +365,16 @@ struct StepPair {
       return Pre{__umul24(c0, K) + c1, 0u, __umul24(c2, K) + c3, 0u};
     }
     if constexpr (DGREP_PAIR_SWZ) x ^= (x >> 1) & 0x30303030u;  // pair_swz of every byte (one v_bitop3)
+    if constexpr (DGREP_PAIR_SDWA0) {
+      // byte 0's table offset 4 * b0 as ONE v_lshlrev_b32_sdwa (hipcc emits
+      // v_lshlrev + v_and for byte 0 while bytes 1-3 get the SDWA form)
+      uint32_t o0;
+      asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+          : "=v"(o0)
+          : "v"(2u), "v"(x));
+      return Pre{*reinterpret_cast<const uint32_t*>(lds + o0), ub_raw((x >> 8) & 0xffu), ua_raw((x >> 16) & 0xffu),
+                 ub_raw(x >> 24)};
+    }
     return Pre{ua_raw(x & 0xffu), ub_raw((x >> 8) & 0xffu), ua_raw((x >> 16) & 0xffu), ub_raw(x >> 24)};
   }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
