@@ -170,6 +170,9 @@ namespace dgrep {
 #ifndef DGREP_FLAT_EMIT
 #define DGREP_FLAT_EMIT 1
 #endif
+#ifndef DGREP_MAX_WG_PER_CU
+#define DGREP_MAX_WG_PER_CU 0
+#endif
 #ifndef DGREP_PAIR_SDWA0
 #define DGREP_PAIR_SDWA0 1
 #endif
@@ -1855,7 +1858,10 @@ hipError_t overflow_t(const ScanArgs& a, uint64_t nover, hipStream_t stream) {
 template <class Step, int TBL>
 hipError_t occ_t(int* b) {
   constexpr int NT = threads_of<Step>();
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL, NT>, NT, 0);
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL, NT>, NT, 0);
+  // DGREP_MAX_WG_PER_CU (tuning, 0 = none): fewer resident lane streams per CU
+  if (DGREP_MAX_WG_PER_CU > 0 && *b > DGREP_MAX_WG_PER_CU) *b = DGREP_MAX_WG_PER_CU;
+  return e;
 }
 
 // One switch for every entry point: stepper by kind, LDS image by size.
