@@ -80,6 +80,10 @@ struct VerifyArgs {
   // DGREP_DFA_PARTIAL blobs: the NFA program (dgrep_blob.h) decides the
   // candidates instead of `full` (verify_nfa_kernel)
   const uint32_t* nfa;
+  // `full` id of the absorbing accepting state (every byte but '\n' loops,
+  // '\n' -> start_m; UINT32_MAX: none): a candidate that reaches it matches,
+  // so verify_kernel stops reading the line there
+  uint32_t matched;
 };
 
 // A staged line whose len has this bit set is a filter CANDIDATE (kStepFilter):

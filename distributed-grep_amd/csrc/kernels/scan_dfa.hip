@@ -1590,7 +1590,7 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
     uint32_t st = v.start;
     for_line_bytes(v.data, a, e, [&](uint32_t b) {
       st = next(st, cls[b]);
-      return true;
+      return st != v.matched;
     });
     return next(st, cn) == v.start_m;
   });

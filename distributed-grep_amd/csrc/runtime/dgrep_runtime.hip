@@ -90,6 +90,7 @@ struct dgrep_ctx {
   bool full_u32 = false;
   uint8_t* d_cls = nullptr;    // [256]
   uint32_t blob_start = 0, blob_start_m = 0;  // start / start_m in d_full's (breadth-first) ids
+  uint32_t blob_matched = UINT32_MAX;          // the absorbing accepting state in d_full's ids (none: UINT32_MAX)
   uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
   uint32_t* d_nfa = nullptr;                   // DGREP_DFA_PARTIAL: the NFA program (verify_nfa_kernel)
   int blocks_per_cu = 1;
@@ -504,6 +505,15 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     HIPCHK(hipMemcpy(c->d_cls, h.byte_class, 256, hipMemcpyHostToDevice));
     c->blob_start = bid[h.start];
     c->blob_start_m = bid[h.start_m];
+    // the absorbing accepting state (MATCHED): verification stops there
+    c->blob_matched = UINT32_MAX;
+    const uint32_t cn = h.byte_class[uint8_t('\n')];
+    for (uint32_t x = 0; x < S && c->blob_matched == UINT32_MAX; ++x) {
+      bool absorbing = trans[size_t(x) * K + cn] == h.start_m;
+      for (uint32_t k = 0; k < K && absorbing; ++k)
+        if (k != cn && trans[size_t(x) * K + k] != x) absorbing = false;
+      if (absorbing) c->blob_matched = bid[x];
+    }
   } else if (h.nstates > 256 || force == 1) {
     if (h.nstates > 65535) {
       c->err = "dgrep_load_dfa: DFA has " + std::to_string(h.nstates) +
@@ -732,6 +742,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.staging_cap = c->staging_cap;
     v.removed = c->d_counters + 3;  // zeroed before the scan
     v.nfa = c->d_nfa;
+    v.matched = c->d_nfa ? UINT32_MAX : c->blob_matched;
     HIPCHK(hipEventRecord(c->ev4, c->stream));
     HIPCHK(verify_candidates(v, c->stream));
     HIPCHK(hipEventRecord(c->ev5, c->stream));
