@@ -33,6 +33,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 STAGED_LINE_BYTES = 16  # StagedLine written by the scan kernel per match
 
 WORKLOADS = {
+    # BASELINE.json configs[0] / SURVEY §8d C1: the reference's CPU-runnable case
+    # (64 MiB, seed 1, 'error'); its cpu_baseline sample covers the whole split
+    "c1": dict(pattern="error", seed=1, kind=0, gib=1 / 16,
+               desc="C1: 64 MiB synthetic log split (seed 1), literal 'error' (the reference's CPU case)"),
     "c2": dict(pattern="error", seed=2, kind=0, gib=16.0,
                desc="C2: 16 GiB synthetic log split (seed 2), literal 'error', LDS-resident DFA"),
     "c2b": dict(pattern="timeout while waiting for lock", seed=2, kind=0, gib=16.0,
