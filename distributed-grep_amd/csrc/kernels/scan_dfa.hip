@@ -170,6 +170,9 @@ namespace dgrep {
 #ifndef DGREP_FLAT_EMIT
 #define DGREP_FLAT_EMIT 1
 #endif
+#ifndef DGREP_FILTER_OPAQUE
+#define DGREP_FILTER_OPAQUE 1
+#endif
 #ifndef DGREP_MAX_WG_PER_CU
 #define DGREP_MAX_WG_PER_CU 0
 #endif
@@ -430,7 +433,13 @@ struct StepFilter {
     return lds[b];  // u8: see kFilterClassBytes
   }
   __device__ __forceinline__ Pre prep(uint32_t x) const {
-    return Pre{cls(x & 0xffu), cls((x >> 8) & 0xffu), cls((x >> 16) & 0xffu), cls(x >> 24)};
+    Pre p{cls(x & 0xffu), cls((x >> 8) & 0xffu), cls((x >> 16) & 0xffu), cls(x >> 24)};
+    if constexpr (DGREP_FILTER_OPAQUE) {
+      // pin the zero-extended loads as 32-bit values: carried across the event
+      // branch as i8, they cost a v_and_b32 0xff each per word
+      asm("" : "+v"(p.c0), "+v"(p.c1), "+v"(p.c2), "+v"(p.c3));
+    }
+    return p;
   }
   __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t c) const {
     return *reinterpret_cast<const uint16_t*>(lds + kFilterClassBytes + 2u * (s + c));
