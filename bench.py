@@ -71,7 +71,10 @@ def log(*a):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU). Without WORLD_SIZE in the environment, N > 1 starts N "
+                         "fresh rank processes under torch.distributed.run; under a launcher it must equal "
+                         "WORLD_SIZE (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
@@ -87,15 +90,57 @@ def parse():
     return ap.parse_args()
 
 
+def free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without a launcher: start N rank processes under
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) as a CHILD
+    process and return its exit code. Nothing here touches the GPU: counting
+    devices does not initialise HIP on this image, and the ranks are fresh
+    processes (never an exec from a process that holds the GPU)."""
+    import subprocess
+
+    import torch
+
+    have = torch.cuda.device_count()
+    if have < args.gpus:
+        log("bench.py --gpus %d: only %d GPU(s) visible; refusing to report an N=%d line" % (args.gpus, have, have))
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        log("bench.py --gpus %d disagrees with WORLD_SIZE=%d" % (args.gpus, world))
+        sys.exit(2)
+    if args.gpus is not None and args.gpus < 1:
+        log("bench.py --gpus must be >= 1")
+        sys.exit(2)
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
     import dgrep
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

@@ -104,11 +104,10 @@ enum : int {
   kStepFilter = 4,  // > 256 states: the DFA's shallow part in LDS, lines that leave it verified afterwards
 };
 
-// LDS image of kStepFilter: byte classes [256] (u8, or u32 with
-// DGREP_FILTER_CLS32), then u16 [state][class] rows of the
-// filter DFA (its states premultiplied by the class count), at most this many
-// bytes in all -- with 1024 threads x 4 slots x 8 B the workgroup stays within
-// the CU's 160 KiB.
+// LDS image of kStepFilter: byte classes [256] (u8), then u16 [state][class]
+// rows of the filter DFA (its states premultiplied by the class count), at
+// most this many bytes in all -- with 1024 threads x 4 slots x 8 B the
+// workgroup stays within the CU's 160 KiB.
 #ifndef DGREP_FILTER_KIB
 #define DGREP_FILTER_KIB 124
 #endif
@@ -117,46 +116,16 @@ constexpr uint32_t kFilterImageBytes = DGREP_FILTER_KIB * 1024;
 // spans 24 dwords in 24 distinct banks and a wave's class reads of text never
 // conflict (tools/lds_bank_bench.hip on the log corpus: u8 table 0 % conflict
 // cycles, u32 entries at 4*b 52 %, u64 at 8*b 55 %). C4 kernel 3.18 -> 3.38 TB/s.
-#ifndef DGREP_FILTER_CLS32
-#define DGREP_FILTER_CLS32 0
-#endif
-constexpr uint32_t kFilterClassBytes = DGREP_FILTER_CLS32 ? 1024 : 256;
+constexpr uint32_t kFilterClassBytes = 256;
 
 // StepPair's two-byte table T2 (u16 [state][class][class], premultiplied
 // states) must address itself with 16-bit values; its whole LDS image (T2 +
-// T1 + the 1 KiB byte table) at most kPairMaxImage bytes.
+// T1 + the 2 KiB of u32 byte tables UA, UB) at most kPairMaxImage bytes.
+// (Byte-table swizzles and a u8 class table were measured slower on MI355X:
+// these steppers are VALU-issue-bound)
 constexpr uint32_t kPairMaxT2 = 32768;
 constexpr uint32_t kPairMaxImage = 40960;
-// DGREP_PAIR_U8: one u8 class table CL[b] = 2*class(b) (256 B, conflict-free
-// over text) and a v_mad_u32_u24 per pair, instead of the u32 UA/UB tables.
-#ifndef DGREP_PAIR_U8
-#define DGREP_PAIR_U8 0
-#endif
-#ifndef DGREP_PAIR_ROWPAD
-#define DGREP_PAIR_ROWPAD 1
-#endif
-constexpr uint32_t kPairT2 = DGREP_PAIR_U8 ? 256 : 2048;  // LDS address of T2 (after the byte tables)
-// DGREP_PAIR_SWZ: UA/UB entry of byte b at index swz(b) = b ^ ((b >> 1) & 0x30)
-// (a bijection). Entry i sits in LDS bank i % 64, so unswizzled the digits
-// 0x30-0x39 share banks with 'p'-'y', '-' ':' '.' with 'm' 'z' 'n'...; swizzled,
-// a wave64 class read over log text costs 1.33 bank cycles instead of 1.97
-// (CPU simulation over the C3 corpus, every swizzle of this form searched).
-// OFF: measured slower on MI355X (C3 kernel 4,030 -> 3,860 GB/s, C2 with
-// DGREP_SHENG_SWZ 5,380 -> 4,820): the two VALU per word the swizzle costs
-// outweigh the bank cycles it saves -- these steppers are VALU-issue-bound.
-#ifndef DGREP_PAIR_SWZ
-#define DGREP_PAIR_SWZ 0
-#endif
-// DGREP_SHENG_SWZ: the same for Sheng8's V[b] (8 bytes: banks 2i, 2i+1 of
-// entry i), swz(b) = b ^ ((b >> 2) & 0x0a): 2.13 bank cycles per read instead
-// of 2.39 on the C2 corpus (simulated)
-#ifndef DGREP_SHENG_SWZ
-#define DGREP_SHENG_SWZ 0
-#endif
-__host__ __device__ constexpr uint32_t sheng_swz(uint32_t b) { return DGREP_SHENG_SWZ ? b ^ ((b >> 2) & 0x0au) : b; }
-__host__ __device__ constexpr uint32_t pair_swz(uint32_t b) {
-  return (DGREP_PAIR_SWZ && !DGREP_PAIR_U8) ? b ^ ((b >> 1) & 0x30u) : b;
-}
+constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the byte tables)
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
 // runtime renumbers states hottest-first (start, start_m, then BFS order from

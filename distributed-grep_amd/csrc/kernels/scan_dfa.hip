@@ -43,17 +43,13 @@
 #include "scan_common.h"
 #include "../../../include/dgrep_blob.h"
 
-// build-time tuning knobs, per stepper (defaults are the shipped
-// configuration, chosen by tools/variant_bench.sh on MI355X):
-//   CHUNK    bytes per lane chunk (multiple of BLOCK)
+// Build-time tuning knobs, per stepper (defaults are the shipped configuration,
+// measured on MI355X; DESIGN.md §3 lists the variants that lost and were removed):
+//   CHUNK    bytes per lane chunk (multiple of BLOCK; the adaptive steppers
+//            start here and double, see adaptive_chunk_bytes)
 //   SLOTS    LDS slots per lane for matching lines
 //   BLOCK    bytes per lane per register load block (64 or 128)
-//   STAGING  1: full tiles are fetched coalesced through LDS (global_load_lds)
 //   WAVES    waves per SIMD the register allocation must allow
-// Sheng (C2, 7 states): direct per-lane loads, 4 KiB chunks, 128-B blocks:
-// 4.16-4.22 TB/s; the staged variant measured 3.5-3.8 TB/s at 1-2 KiB chunks.
-// Table (C3, 20 states): two 2 KiB chunks per lane stepped in lockstep, direct
-// loads: 2.94 TB/s (one chunk staged 2.83, direct 2.67).
 #ifndef DGREP_SHENG_CHUNK
 #define DGREP_SHENG_CHUNK 4096
 #endif
@@ -63,44 +59,22 @@
 #ifndef DGREP_SHENG_BLOCK
 #define DGREP_SHENG_BLOCK 128
 #endif
-#ifndef DGREP_SHENG_STAGING
-#define DGREP_SHENG_STAGING 0
+#ifndef DGREP_SHENG_WAVES
+#define DGREP_SHENG_WAVES 3
 #endif
+// Table (<= 256 states not fitting Pair): two 2 KiB chunks per lane stepped in
+// lockstep while the table is small (<= 64 states)
 #ifndef DGREP_TABLE_CHUNK
 #define DGREP_TABLE_CHUNK 2048
 #endif
 #ifndef DGREP_TABLE_SLOTS
 #define DGREP_TABLE_SLOTS 6
 #endif
-#ifndef DGREP_TABLE_STAGING
-#define DGREP_TABLE_STAGING 0
-#endif
-#ifndef DGREP_SHENG_STREAMS
-#define DGREP_SHENG_STREAMS 1
-#endif
-#ifndef DGREP_TABLE_STREAMS
-#define DGREP_TABLE_STREAMS 2
-#endif
-#ifndef DGREP_WIDE_STREAMS
-#define DGREP_WIDE_STREAMS 1
-#endif
-#ifndef DGREP_SHENG_WAVES
-#define DGREP_SHENG_WAVES 3
+#ifndef DGREP_TABLE_BLOCK
+#define DGREP_TABLE_BLOCK 64
 #endif
 #ifndef DGREP_TABLE_WAVES
 #define DGREP_TABLE_WAVES 3
-#endif
-// staged rounds in flight per wave (1: the next round is fetched while one is
-// stepped; 2: two rounds ahead, double the LDS ring)
-#ifndef DGREP_STAGE_DEPTH
-#define DGREP_STAGE_DEPTH 1
-#endif
-// bytes per lane per staged round (global_load_lds path); 128 = whole lines
-#ifndef DGREP_STAGE_ROUND
-#define DGREP_STAGE_ROUND 128
-#endif
-#ifndef DGREP_TABLE_BLOCK
-#define DGREP_TABLE_BLOCK 64
 #endif
 #ifndef DGREP_WIDE_CHUNK
 #define DGREP_WIDE_CHUNK 1024
@@ -111,33 +85,12 @@
 #ifndef DGREP_WIDE_BLOCK
 #define DGREP_WIDE_BLOCK 64
 #endif
-// non-temporal split loads per stepper (see load_block)
-#ifndef DGREP_NT_WIDE
-#define DGREP_NT_WIDE 0
-#endif
-#ifndef DGREP_NT_TABLE
-#define DGREP_NT_TABLE 0
-#endif
-#ifndef DGREP_NT_SHENG
-#define DGREP_NT_SHENG 0
-#endif
 // Pair (C3, 20 states): one chunk per lane, runtime (adaptive) chunk from 4 KiB
 #ifndef DGREP_PAIR_CHUNK
 #define DGREP_PAIR_CHUNK 4096
 #endif
-// deferred events (run_block_defer) for the pair stepper; its per-lane LDS
-// park area (128 B) leaves room for 4 slots per lane (the rest spill to HBM)
-#ifndef DGREP_DEFER
-#define DGREP_DEFER 0
-#endif
-#ifndef DGREP_DEFER_LAZY
-#define DGREP_DEFER_LAZY 1
-#endif
-#ifndef DGREP_DEFER_PAIRREAD
-#define DGREP_DEFER_PAIRREAD 1
-#endif
 #ifndef DGREP_PAIR_SLOTS
-#define DGREP_PAIR_SLOTS (DGREP_DEFER ? 4 : 16)
+#define DGREP_PAIR_SLOTS 16
 #endif
 #ifndef DGREP_PAIR_BLOCK
 #define DGREP_PAIR_BLOCK 128
@@ -155,60 +108,29 @@
 #ifndef DGREP_FILTER_BLOCK
 #define DGREP_FILTER_BLOCK 128
 #endif
-#ifndef DGREP_SHENG_SCHED_BARRIER
-#define DGREP_SHENG_SCHED_BARRIER 0
-#endif
 
 namespace dgrep {
 
-
-// DGREP_FLAT_EMIT: the event fast path of the one-stream slot steppers writes
-// its record branch-free -- to LDS slot min(nev, E), slot E being a per-lane
-// dummy, and bumps nev only if the lane owns the line -- instead of nesting
-// exec-mask regions for ownership and slot-vs-spill (the spill write stays a
-// branch, almost always skipped by the whole wave)
-#ifndef DGREP_FLAT_EMIT
-#define DGREP_FLAT_EMIT 1
-#endif
-#ifndef DGREP_FILTER_OPAQUE
-#define DGREP_FILTER_OPAQUE 1
-#endif
-#ifndef DGREP_MAX_WG_PER_CU
-#define DGREP_MAX_WG_PER_CU 0
-#endif
-#ifndef DGREP_PAIR_SDWA0
-#define DGREP_PAIR_SDWA0 1
-#endif
-// DGREP_NL_ASM: the last op of nl_mask and the '\n' count as inline asm, so
-// the compiler neither re-derives "m != 0" from the mask's inputs (it
-// canonicalised that test into v_bitop3 + v_cmp instead of one v_cmp on m) nor
-// splits popcount + sum into v_bcnt + v_add (v_bcnt_u32_b32 accumulates):
-// two VALU fewer per word on the per-word steppers, which are VALU-issue-bound.
-#ifndef DGREP_NL_ASM
-#define DGREP_NL_ASM 1
-#endif
+// nl_mask: the last op as inline asm, so the compiler neither re-derives
+// "m != 0" from the mask's inputs (it canonicalised that test into v_bitop3 +
+// v_cmp instead of one v_cmp on m) nor splits popcount + sum into v_bcnt +
+// v_add (v_bcnt_u32_b32 accumulates): two VALU fewer per word on the per-word
+// steppers, which are VALU-issue-bound.
 __device__ __forceinline__ uint32_t nl_mask(uint32_t w) {
   // exact per-byte zero test of w ^ '\n\n\n\n': bit 7 of byte k set iff byte k == '\n'
-  uint32_t x = w ^ 0x0a0a0a0au;
-  if constexpr (DGREP_NL_ASM) {
-    const uint32_t t = (x & 0x7f7f7f7fu) + 0x7f7f7f7fu;
-    uint32_t m;
-    // m = ~(t | w) & 0x80808080 (bit 7 of w equals bit 7 of x); truth table
-    // index = (S0 << 2) | (S1 << 1) | S2: true only at S0 = S1 = 0, S2 = 1
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:2" : "=v"(m) : "v"(t), "v"(w), "s"(0x80808080u));
-    return m;
-  }
-  uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
-  return ~t & 0x80808080u;
+  const uint32_t x = w ^ 0x0a0a0a0au;
+  const uint32_t t = (x & 0x7f7f7f7fu) + 0x7f7f7f7fu;
+  uint32_t m;
+  // m = ~(t | w) & 0x80808080 (bit 7 of w equals bit 7 of x); truth table
+  // index = (S0 << 2) | (S1 << 1) | S2: true only at S0 = S1 = 0, S2 = 1
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:2" : "=v"(m) : "v"(t), "v"(w), "s"(0x80808080u));
+  return m;
 }
 // acc + popcount(m) in one v_bcnt_u32_b32
 __device__ __forceinline__ uint32_t add_popc(uint32_t acc, uint32_t m) {
-  if constexpr (DGREP_NL_ASM) {
-    uint32_t r;
-    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(m), "v"(acc));
-    return r;
-  }
-  return acc + uint32_t(__popc(m));
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(m), "v"(acc));
+  return r;
 }
 __device__ __forceinline__ uint32_t hi_byte(uint32_t m) { return (31u - __clz(m)) >> 3; }
 
@@ -261,7 +183,6 @@ struct StepSheng8 {
     uint2 m0, m1, m2, m3;
   };
   __device__ __forceinline__ Pre prep(uint32_t x) const {
-    if constexpr (DGREP_SHENG_SWZ) x ^= (x >> 2) & 0x0a0a0a0au;  // sheng_swz of every byte
     return Pre{V[x & 0xffu], V[(x >> 8) & 0xffu], V[(x >> 16) & 0xffu], V[x >> 24]};
   }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
@@ -271,27 +192,12 @@ struct StepSheng8 {
     s2 = sel(p.m2, s1);
     s3 = sel(p.m3, s2);
   }
-  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[sheng_swz(b)], s); }
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return sel(V[b], s); }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return (s & 0xffu) == M; }
   // states are replicated bytes and start_m is the highest state (host
   // renumbering): one max over the word's four states replaces four compares
   __device__ __forceinline__ static bool any4(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t M) {
     return max(max(s0, s1), max(s2, s3)) >= M * 0x01010101u;
-  }
-  // map <- transitions of bytes 0..lim of the word applied to the 8-state map
-  // (lo: states 0-3, hi: states 4-7); one v_perm per byte and half
-  __device__ __forceinline__ void compose(const Pre& p, uint32_t lim, uint32_t& lo, uint32_t& hi) const {
-    lo = sel(p.m0, lo);
-    hi = sel(p.m0, hi);
-    const uint32_t l1 = sel(p.m1, lo), h1 = sel(p.m1, hi);
-    lo = lim >= 1 ? l1 : lo;
-    hi = lim >= 1 ? h1 : hi;
-    const uint32_t l2 = sel(p.m2, lo), h2 = sel(p.m2, hi);
-    lo = lim >= 2 ? l2 : lo;
-    hi = lim >= 2 ? h2 : hi;
-    const uint32_t l3 = sel(p.m3, lo), h3 = sel(p.m3, hi);
-    lo = lim >= 3 ? l3 : lo;
-    hi = lim >= 3 ? h3 : hi;
   }
 };
 
@@ -355,33 +261,20 @@ struct StepPair {
   struct Pre {
     uint32_t a0, b1, a2, b3;
   };
-  // raw: b is already swizzled (pair_swz)
-  __device__ __forceinline__ uint32_t ua_raw(uint32_t b) const {
+  __device__ __forceinline__ uint32_t ua(uint32_t b) const {
     return *reinterpret_cast<const uint32_t*>(lds + 4u * b);
   }
-  __device__ __forceinline__ uint32_t ub_raw(uint32_t b) const {
-    if constexpr (DGREP_PAIR_U8) return lds[b];  // CL[b] = 2 * class(b)
+  __device__ __forceinline__ uint32_t ub(uint32_t b) const {
     return *reinterpret_cast<const uint32_t*>(lds + 1024u + 4u * b);
   }
-  __device__ __forceinline__ uint32_t ub(uint32_t b) const { return ub_raw(pair_swz(b)); }
   __device__ __forceinline__ Pre prep(uint32_t x) const {
-    if constexpr (DGREP_PAIR_U8) {
-      // a0 = 2K*c0 + 2*c1, a2 = 2K*c2 + 2*c3 (b1 = b3 = 0)
-      const uint32_t c0 = lds[x & 0xffu], c1 = lds[(x >> 8) & 0xffu], c2 = lds[(x >> 16) & 0xffu], c3 = lds[x >> 24];
-      return Pre{__umul24(c0, K) + c1, 0u, __umul24(c2, K) + c3, 0u};
-    }
-    if constexpr (DGREP_PAIR_SWZ) x ^= (x >> 1) & 0x30303030u;  // pair_swz of every byte (one v_bitop3)
-    if constexpr (DGREP_PAIR_SDWA0) {
-      // byte 0's table offset 4 * b0 as ONE v_lshlrev_b32_sdwa (hipcc emits
-      // v_lshlrev + v_and for byte 0 while bytes 1-3 get the SDWA form)
-      uint32_t o0;
-      asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
-          : "=v"(o0)
-          : "v"(2u), "v"(x));
-      return Pre{*reinterpret_cast<const uint32_t*>(lds + o0), ub_raw((x >> 8) & 0xffu), ua_raw((x >> 16) & 0xffu),
-                 ub_raw(x >> 24)};
-    }
-    return Pre{ua_raw(x & 0xffu), ub_raw((x >> 8) & 0xffu), ua_raw((x >> 16) & 0xffu), ub_raw(x >> 24)};
+    // byte 0's table offset 4 * b0 as ONE v_lshlrev_b32_sdwa (hipcc emits
+    // v_lshlrev + v_and for byte 0 while bytes 1-3 get the SDWA form)
+    uint32_t o0;
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+        : "=v"(o0)
+        : "v"(2u), "v"(x));
+    return Pre{*reinterpret_cast<const uint32_t*>(lds + o0), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu), ub(x >> 24)};
   }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
     return *reinterpret_cast<const uint16_t*>(lds + off);
@@ -428,17 +321,12 @@ struct StepFilter {
   struct Pre {
     uint32_t c0, c1, c2, c3;
   };
-  __device__ __forceinline__ uint32_t cls(uint32_t b) const {
-    if constexpr (DGREP_FILTER_CLS32) return *reinterpret_cast<const uint32_t*>(lds + 4u * b);
-    return lds[b];  // u8: see kFilterClassBytes
-  }
+  __device__ __forceinline__ uint32_t cls(uint32_t b) const { return lds[b]; }  // u8: see kFilterClassBytes
   __device__ __forceinline__ Pre prep(uint32_t x) const {
     Pre p{cls(x & 0xffu), cls((x >> 8) & 0xffu), cls((x >> 16) & 0xffu), cls(x >> 24)};
-    if constexpr (DGREP_FILTER_OPAQUE) {
-      // pin the zero-extended loads as 32-bit values: carried across the event
-      // branch as i8, they cost a v_and_b32 0xff each per word
-      asm("" : "+v"(p.c0), "+v"(p.c1), "+v"(p.c2), "+v"(p.c3));
-    }
+    // pin the zero-extended loads as 32-bit values: carried across the event
+    // branch as i8, they cost a v_and_b32 0xff each per word
+    asm("" : "+v"(p.c0), "+v"(p.c1), "+v"(p.c2), "+v"(p.c3));
     return p;
   }
   __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t c) const {
@@ -490,15 +378,15 @@ struct Tune;
 // S = chunks per lane (1, or 2 stepped in lockstep by run_lane2)
 template <>
 struct Tune<StepSheng8> {
-  static constexpr int C = DGREP_SHENG_CHUNK, E = DGREP_SHENG_SLOTS, B = DGREP_SHENG_BLOCK, S = DGREP_SHENG_STREAMS;
+  static constexpr int C = DGREP_SHENG_CHUNK, E = DGREP_SHENG_SLOTS, B = DGREP_SHENG_BLOCK, S = 1;
 };
 template <>
 struct Tune<StepTable> {
-  static constexpr int C = DGREP_TABLE_CHUNK, E = DGREP_TABLE_SLOTS, B = DGREP_TABLE_BLOCK, S = DGREP_TABLE_STREAMS;
+  static constexpr int C = DGREP_TABLE_CHUNK, E = DGREP_TABLE_SLOTS, B = DGREP_TABLE_BLOCK, S = 2;
 };
 template <>
 struct Tune<StepWide> {
-  static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK, S = DGREP_WIDE_STREAMS;
+  static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK, S = 1;
 };
 template <>
 struct Tune<StepFilter> {
@@ -538,13 +426,6 @@ struct LaneRun {
   bool seen;         // a line boundary has been crossed (owned lines begin)
   bool term;         // the terminating '\n' at or after the chunk end was consumed
   uint32_t nev;      // matching lines emitted
-  // Sheng staged path: transition map (byte s = state reached from state s) of
-  // the chunk's bytes up to and including its first '\n', and that '\n''s
-  // position (-1: not seen yet). The left neighbour lane finishes its last
-  // owned line with it instead of reading this chunk again.
-  uint32_t mlo, mhi;
-  int32_t p1;
-  int32_t pend;      // deferred path: position of the word holding the last '\n' (-1: resolved)
 };
 
 template <int E, bool DIRECT>
@@ -604,9 +485,6 @@ struct Emitter {
   }
   __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
     const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
-#ifdef DGREP_ABLATE_EMIT
-    if (DGREP_ABLATE_EMIT) { r.nev += (lw == 0xffffffffu); return; }  // ablation build only (wrong results)
-#endif
     if (DIRECT) {
       const uint64_t o = out_base + r.nev;
       if (o < a->capacity) {
@@ -643,28 +521,27 @@ struct Blk {
 template <class Step, bool DIRECT>
 constexpr bool flat_emit() {
   // (not Filter: its 1024 threads x 8 B dummy would not fit beside its 124 KiB image)
-  return DGREP_FLAT_EMIT && !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair);
+  return !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair);
 }
 
 // Everything a word step does after its four DFA steps s0..s3 (newline mask
-// m): matching-line events, the first-piece map (TRACK), newline bookkeeping.
-template <int J, bool TRACK, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
-                                            uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
+// m): matching-line events, newline bookkeeping.
+template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
+                                            uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit);
 
-template <int J, bool TRACK, class Step, int E, bool DIRECT>
+template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x, const typename Step::Pre& pre,
                                           uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   // StepTable: keep each word's work in place (hoisting the chain-independent
   // newline masks of a whole block costs ~100 VGPRs). StepSheng8 wants the
   // opposite: its state-independent LDS reads should run ahead of the chain.
-  if ((Step::kKind != kStepSheng8 && Step::kKind != kStepPair) || DGREP_SHENG_SCHED_BARRIER)
-    __builtin_amdgcn_sched_barrier(0);
+  if (Step::kKind != kStepSheng8 && Step::kKind != kStepPair) __builtin_amdgcn_sched_barrier(0);
   const uint32_t m = nl_mask(x);
   uint32_t s0, s1, s2, s3;
   st.apply(pre, s, s0, s1, s2, s3);
-  word_events<J, TRACK>(st, M, m, pre, s0, s1, s2, s3, b, r, emit);
+  word_events<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
   s = s3;
 }
 
@@ -680,8 +557,8 @@ __device__ __forceinline__ void word_step2(const Step& st, uint32_t M, uint32_t 
   uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
   st.apply(pa, sa, a0, a1, a2, a3);
   st.apply(pb, sb, b0, b1, b2, b3);
-  word_events<J, false>(st, M, ma, pa, a0, a1, a2, a3, ba, ra, ea);
-  word_events<J, false>(st, M, mb, pb, b0, b1, b2, b3, bb, rb, eb);
+  word_events<J>(st, M, ma, a0, a1, a2, a3, ba, ra, ea);
+  word_events<J>(st, M, mb, b0, b1, b2, b3, bb, rb, eb);
   sa = a3;
   sb = b3;
 }
@@ -691,10 +568,6 @@ __device__ __forceinline__ void word_step2(const Step& st, uint32_t M, uint32_t 
 template <class Step>
 __device__ __forceinline__ bool word_any(const Step& st, uint32_t M, uint32_t s0, uint32_t s1, uint32_t s2,
                                          uint32_t s3) {
-#ifdef DGREP_ABLATE_EVENTS
-  // ablation build only (wrong results): no event is ever taken, same DFA
-  if (DGREP_ABLATE_EVENTS) return false;
-#endif
   if constexpr (Step::kKind == kStepSheng8)
     return StepSheng8::any4(s0, s1, s2, s3, M);
   else if constexpr (Step::kKind == kStepPair)
@@ -758,57 +631,12 @@ __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
   if (m) { b.lastm = m; b.lastj = J; }
 }
 
-template <int J, bool TRACK, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, const typename Step::Pre& pre,
-                                            uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
+template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
+                                            uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
   if (__builtin_expect(word_any(st, M, s0, s1, s2, s3), 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
-  if constexpr (TRACK) {
-    if (r.p1 < 0) {
-      // the chunk's first line piece: compose its transition map (LaneRun::mlo)
-      const uint32_t lim = m ? uint32_t(__builtin_ctz(m)) >> 3 : 3u;
-      st.compose(pre, lim, r.mlo, r.mhi);
-      if (m) r.p1 = int32_t(b.pos + 4u * J + lim);
-    }
-  }
   word_nl<J>(m, b);
-}
-
-// Four words J..J+3 (J % 4 == 0) of a block: their DFA steps (each word's
-// state-independent prep still issued one word ahead), then ONE wave-uniform
-// event test for the 16 bytes -- inside it the words are resolved in order,
-// each with the bookkeeping of the words before it -- then the newline
-// bookkeeping. The event branch is entered once per 16 bytes instead of once
-// per word that holds an event in any of the wave's 64 lanes.
-template <int J, int NW, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void quad_step(const Step& st, uint32_t M, const uint32_t (&w)[NW],
-                                          typename Step::Pre& pre, uint32_t& s, Blk& b, LaneRun& r,
-                                          const Emitter<E, DIRECT>& emit) {
-  uint32_t q[4][4], m[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const typename Step::Pre cur = pre;
-    if (J + i + 1 < NW) pre = st.prep(w[J + i + 1 < NW ? J + i + 1 : 0]);
-    m[i] = nl_mask(w[J + i]);
-    st.apply(cur, s, q[i][0], q[i][1], q[i][2], q[i][3]);
-    s = q[i][3];
-  }
-  bool any = false;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) any = any | word_any(st, M, q[i][0], q[i][1], q[i][2], q[i][3]);
-  if (__builtin_expect(any, 0)) {
-    Blk t = b;
-#define DG_QE(I)                                                                     \
-  if (word_any(st, M, q[I][0], q[I][1], q[I][2], q[I][3]))                           \
-    word_emit<J + (I)>(st, M, m[I], q[I][0], q[I][1], q[I][2], q[I][3], t, r, emit); \
-  word_nl<J + (I)>(m[I], t);
-    DG_QE(0) DG_QE(1) DG_QE(2) DG_QE(3)
-#undef DG_QE
-  }
-  word_nl<J>(m[0], b);
-  word_nl<J + 1>(m[1], b);
-  word_nl<J + 2>(m[2], b);
-  word_nl<J + 3>(m[3], b);
 }
 
 __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const LaneRun& r) {
@@ -871,21 +699,7 @@ __device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uin
   blk_finish(bb, sb, rb);
 }
 
-// Event tests per 16 bytes (quad_step) for the steppers whose steps run ahead
-// of their bookkeeping; the u8 table (sched barriers per word, VGPR-bound) and
-// the wide stepper keep one test per word, as does the staged Sheng path (TRACK).
-// (measured on C3 / Pair: 3,644 GB/s with quads vs 3,699 without -- the extra
-// live states cost more than the saved branches; off by default)
-#ifndef DGREP_QUADS
-#define DGREP_QUADS 0
-#endif
-template <class Step, bool TRACK>
-constexpr bool use_quads() {
-  return DGREP_QUADS && !TRACK &&
-         Step::kKind == kStepPair;
-}
-
-template <int BK, bool TRACK = false, class Step, int E, bool DIRECT>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
@@ -902,168 +716,27 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
     w[4 * i + 3] = v[i].w;
   }
   typename Step::Pre pre = st.prep(w[0]);
-  if constexpr (use_quads<Step, TRACK>()) {
-#define DG_Q(J) \
-  if ((J) < NW) quad_step<((J) < NW ? (J) : 0)>(st, M, w, pre, s, b, r, emit);
-    DG_Q(0) DG_Q(4) DG_Q(8) DG_Q(12) DG_Q(16) DG_Q(20) DG_Q(24) DG_Q(28)
-#undef DG_Q
-  } else {
 #define DG_W(J)                                                                         \
   if ((J) < NW) {                                                                       \
     const typename Step::Pre cur = pre;                                                 \
     if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : 0]);                     \
-    word_step<J, TRACK>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit);              \
+    word_step<J>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit);                     \
   }
-    DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
-    DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
-    DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
-    DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
+  DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
+  DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
+  DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
+  DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
 #undef DG_W
-  }
   blk_finish(b, s, r);
 }
 
-// Deferred events (Pair stepper). The per-word event branch of run_block is
-// entered whenever ANY of the wave's 64 lanes ends a matching line in that
-// word (C3, 15 % matching lines: about 27 % of all words), and each entry runs
-// its whole emit path for one or two active lanes. Here a block's 32 words are
-// stepped with no branch at all: each word only shifts two bits into per-lane
-// masks -- `evb` (the word ends a matching line) and `hb` (the word holds a
-// '\n') -- and counts its '\n'. The block's raw words are parked in this lane's
-// LDS area, and after the block each lane walks only its OWN event words
-// (about 1.5 iterations per block for the wave instead of ~9 branch entries),
-// re-reading the event word and the previous '\n' word from the park. A word
-// with two or more '\n' breaks the one-'\n'-per-word arithmetic (nls !=
-// popc(hb)); a lane with such a word and an event in the block re-runs the
-// block on the exact per-word path, as does every block past the chunk end.
-// Park layout: 16-B piece i of the block at 16 * (i ^ ((lane >> 1) & 7)),
-// which keeps the ds_write_b128 of all 64 lanes bank-conflict-free.
-template <class Step>
-constexpr bool use_defer() {
-  return DGREP_DEFER && Step::kKind == kStepPair;
-}
-__device__ __forceinline__ uint32_t park_word(const uint8_t* park, uint32_t psw, uint32_t j) {
-  return *reinterpret_cast<const uint32_t*>(park + 16u * ((j >> 2) ^ psw) + 4u * (j & 3u));
-}
-// r.prev_nl of a deferred block whose last '\n' sits in word `r.pend` (block
-// position + 4 * word) of the park: read it before the park is overwritten
+// Split loads: BK bytes of one lane, 16 B per load (through L2: non-temporal
+// loads measured ~2x slower, the per-lane 16-B pieces of a 128-B line rely on it)
 template <int BK>
-__device__ __forceinline__ void defer_resolve(LaneRun& r, const uint8_t* park, uint32_t psw) {
-  // branch-free: the read stays in the block's basic block, its use sinks
-  const uint32_t x = park_word(park, psw, (uint32_t(r.pend) & uint32_t(BK - 1)) >> 2);
-  const int64_t q = int64_t(uint32_t(r.pend) + hi_byte(nl_mask(x)));
-  r.prev_nl = r.pend >= 0 ? q : r.prev_nl;
-  r.pend = -1;
-}
-template <int BK, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void run_block_defer(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
-                                                uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit, uint8_t* park,
-                                                uint32_t psw) {
-  defer_resolve<BK>(r, park, psw);
-  if (pos >= C) {  // wave-uniform (every lane of a tile steps the same block offsets)
-    run_block<BK>(st, M, v, pos, C, r, emit);
-    return;
-  }
-  constexpr int NW = BK / 4;
-#pragma unroll
-  for (int i = 0; i < BK / 16; ++i) *reinterpret_cast<uint4*>(park + 16u * (uint32_t(i) ^ psw)) = v[i];
-  uint32_t w[NW];
-#pragma unroll
-  for (int i = 0; i < BK / 16; ++i) {
-    w[4 * i + 0] = v[i].x;
-    w[4 * i + 1] = v[i].y;
-    w[4 * i + 2] = v[i].z;
-    w[4 * i + 3] = v[i].w;
-  }
-  uint32_t s = r.s, evb = 0, hb = 0, nls = 0;
-  typename Step::Pre pre = st.prep(w[0]);
-#pragma unroll
-  for (int j = 0; j < NW; ++j) {
-    const typename Step::Pre cur = pre;
-    if (j + 1 < NW) pre = st.prep(w[j + 1 < NW ? j + 1 : 0]);
-    const uint32_t m = nl_mask(w[j]);
-    uint32_t s0, s1, s2, s3;
-    st.apply(cur, s, s0, s1, s2, s3);
-    s = s3;
-    nls = add_popc(nls, m);
-    hb = (hb << 1) | uint32_t(m != 0u);
-    evb = (evb << 1) | uint32_t(word_any(st, M, s0, s1, s2, s3));
-  }
-  // word j sits at bit NW-1-j of evb / hb
-  if (evb != 0u && nls != uint32_t(__popc(hb))) {
-    // exact path from the block's start state, over the parked words (the
-    // block's registers are dead by now)
-    uint4 u[BK / 16];
-#pragma unroll
-    for (int i = 0; i < BK / 16; ++i) u[i] = *reinterpret_cast<const uint4*>(park + 16u * (uint32_t(i) ^ psw));
-    run_block<BK>(st, M, u, pos, C, r, emit);
-    return;
-  }
-  const uint32_t p32 = uint32_t(pos);
-  while (evb) {
-    const uint32_t jb = 31u - uint32_t(__clz(evb));  // highest bit = lowest word
-    evb &= ~(1u << jb);
-    const uint32_t j = uint32_t(NW - 1) - jb;
-    const uint32_t hp = jb + 1u < 32u ? hb >> (jb + 1u) : 0u;  // words 0..j-1 (word j-1 at bit 0)
-    if constexpr (DGREP_DEFER_PAIRREAD) {
-      // both park reads issued together (one LDS round trip): the event word
-      // and the word of the previous '\n' (a harmless re-read of word j if none)
-      const uint32_t jp = hp ? j - 1u - uint32_t(__builtin_ctz(hp)) : j;
-      const uint32_t x = park_word(park, psw, j), y = park_word(park, psw, jp);
-      const uint32_t k = uint32_t(__builtin_ctz(nl_mask(x))) >> 3;  // exactly one '\n': the event
-      const uint32_t prev = hp ? p32 + 4u * jp + hi_byte(nl_mask(y)) : uint32_t(r.prev_nl);
-      if (hp || r.seen) emit.inner(r, p32 + 4u * j + k, prev + 1u, r.nl + uint32_t(__popc(hp)), false);
-    } else {
-      const uint32_t m = nl_mask(park_word(park, psw, j));  // exactly one '\n': the event
-      const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
-      uint32_t prev;
-      bool own;
-      if (hp) {
-        const uint32_t jp = j - 1u - uint32_t(__builtin_ctz(hp));
-        prev = p32 + 4u * jp + hi_byte(nl_mask(park_word(park, psw, jp)));
-        own = true;
-      } else {
-        prev = uint32_t(r.prev_nl);
-        own = r.seen;
-      }
-      if (own) emit.inner(r, p32 + 4u * j + k, prev + 1u, r.nl + uint32_t(__popc(hp)), false);
-    }
-  }
-  r.s = s;
-  r.nl += nls;
-  if (hb) {
-    const uint32_t jl = uint32_t(NW - 1) - uint32_t(__builtin_ctz(hb));
-    if constexpr (DGREP_DEFER_LAZY) {
-      // the block's last '\n' (the next line's start) is resolved at the next
-      // block's entry (defer_resolve), where its park read overlaps the stepping
-      r.pend = int32_t(p32 + 4u * jl);
-    } else {
-      r.prev_nl = int64_t(p32 + 4u * jl + hi_byte(nl_mask(park_word(park, psw, jl))));
-    }
-    r.seen = true;
-  }
-}
-
-// Split loads. NT: non-temporal (streaming) loads, so the once-read split does
-// not evict what must stay in L2 (the wide stepper's cold table rows).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-template <int BK, bool NT = false>
 __device__ __forceinline__ void load_block(uint4 (&v)[BK / 16], const uint8_t* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-  for (int i = 0; i < BK / 16; ++i) {
-    if constexpr (NT) {
-      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q) + i);
-      v[i] = make_uint4(x.x, x.y, x.z, x.w);
-    } else {
-      v[i] = q[i];
-    }
-  }
-}
-template <class Step>
-constexpr bool nt_loads() {
-  return (Step::kKind == kStepWide && DGREP_NT_WIDE) || (Step::kKind == kStepTable && DGREP_NT_TABLE) ||
-         (Step::kKind == kStepSheng8 && DGREP_NT_SHENG);
+  for (int i = 0; i < BK / 16; ++i) v[i] = q[i];
 }
 
 // The last < BLOCK bytes of the split, one byte at a time, then the end of the
@@ -1096,32 +769,15 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
   r.seen = (cs == 0);
   r.term = false;
   r.nev = 0;
-  r.mlo = 0x03020100u;  // identity map
-  r.mhi = 0x07060504u;
-  r.p1 = -1;
-  r.pend = -1;
 }
 
 // Runs a lane (see file comment) from chunk-relative position pos0 over
 // BK-byte blocks with direct per-lane loads, prefetching the next block while
 // the current one is stepped (two register buffers, ping-pong). Returns the
 // number of '\n' inside the lane's own chunk [cs, cs + C).
-template <int BK, bool DEFER = false, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void step_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
-                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit, uint8_t* park,
-                                           uint32_t psw) {
-  if constexpr (DEFER)
-    run_block_defer<BK>(st, M, v, pos, C, r, emit, park, psw);
-  else
-    run_block<BK>(st, M, v, pos, C, r, emit);
-}
-
-// DEFER: blocks inside the chunk go through run_block_defer (park: this lane's
-// BK-byte LDS area, psw its piece swizzle)
-template <int BK, bool DEFER = false, class Step, int E, bool DIRECT>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step& st, uint64_t cs, uint64_t pos0,
-                                                  LaneRun& r, const Emitter<E, DIRECT>& emit, const uint32_t C,
-                                                  uint8_t* park = nullptr, uint32_t psw = 0) {
+                                                  LaneRun& r, const Emitter<E, DIRECT>& emit, const uint32_t C) {
   const uint32_t M = a.start_m;
   const uint64_t avail = cs < a.n ? a.n - cs : 0;
   if (avail <= pos0) {
@@ -1135,42 +791,38 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   bool snap = false;
   uint64_t pos = pos0;
   uint4 A[BK / 16], B[BK / 16];
-  if (pos0 + BK <= avail) load_block<BK, nt_loads<Step>()>(A, p + pos0);
+  if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
   for (;;) {
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
     if (pos + BK > avail) {
-      if constexpr (DEFER) defer_resolve<BK>(r, park, psw);
       run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);
       break;
     }
-    load_block<BK, nt_loads<Step>()>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
-    step_block<BK, DEFER>(st, M, A, pos, uint64_t(C), r, emit, park, psw);
+    load_block<BK>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
+    run_block<BK>(st, M, A, pos, uint64_t(C), r, emit);
     pos += BK;
 
     if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
     if (pos >= uint64_t(C) && r.term) break;
     if (pos + BK > avail) {
-      if constexpr (DEFER) defer_resolve<BK>(r, park, psw);
       run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);
       break;
     }
-    load_block<BK, nt_loads<Step>()>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
-    step_block<BK, DEFER>(st, M, B, pos, uint64_t(C), r, emit, park, psw);
+    load_block<BK>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
+    run_block<BK>(st, M, B, pos, uint64_t(C), r, emit);
     pos += BK;
   }
-  if constexpr (DEFER) defer_resolve<BK>(r, park, psw);
   if (!snap) nl_chunk = r.nl;
   return nl_chunk;
 }
 
-template <int BK, bool DEFER = false, class Step, int E, bool DIRECT>
+template <int BK, class Step, int E, bool DIRECT>
 __device__ __forceinline__ uint32_t run_lane(const ScanArgs& a, const Step& st, uint64_t cs, LaneRun& r,
-                                             const Emitter<E, DIRECT>& emit, const uint32_t C,
-                                             uint8_t* park = nullptr, uint32_t psw = 0) {
+                                             const Emitter<E, DIRECT>& emit, const uint32_t C) {
   lane_init(a, cs, r);
   if (cs >= a.n) return 0;
-  return run_lane_from<BK, DEFER>(a, st, cs, 0, r, emit, C, park, psw);
+  return run_lane_from<BK>(a, st, cs, 0, r, emit, C);
 }
 
 // Two chunks per lane (csa, csb), both wholly inside the split, stepped in
@@ -1187,15 +839,15 @@ __device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uin
   const uint8_t* pa = a.data + csa;
   const uint8_t* pb = a.data + csb;
   uint4 A0[BK / 16], A1[BK / 16], B0[BK / 16], B1[BK / 16];
-  load_block<BK, nt_loads<Step>()>(A0, pa);
-  load_block<BK, nt_loads<Step>()>(B0, pb);
+  load_block<BK>(A0, pa);
+  load_block<BK>(B0, pb);
   for (uint32_t pos = 0; pos < uint32_t(C); pos += 2 * BK) {
-    load_block<BK, nt_loads<Step>()>(A1, pa + pos + BK);
-    load_block<BK, nt_loads<Step>()>(B1, pb + pos + BK);
+    load_block<BK>(A1, pa + pos + BK);
+    load_block<BK>(B1, pb + pos + BK);
     run_block2<BK>(st, M, A0, B0, pos, uint64_t(C), ra, rb, ea, eb);
     if (pos + 2 * BK < uint32_t(C)) {
-      load_block<BK, nt_loads<Step>()>(A0, pa + pos + 2 * BK);
-      load_block<BK, nt_loads<Step>()>(B0, pb + pos + 2 * BK);
+      load_block<BK>(A0, pa + pos + 2 * BK);
+      load_block<BK>(B0, pb + pos + 2 * BK);
     }
     run_block2<BK>(st, M, A1, B1, pos + BK, uint64_t(C), ra, rb, ea, eb);
   }
@@ -1205,106 +857,16 @@ __device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uin
   run_lane_from<BK>(a, st, csb, uint64_t(C), rb, eb, uint32_t(C));
 }
 
-// 16 bytes global -> LDS (global_load_lds_dwordx4); the LDS destination is
-// the wave-uniform `lds` + lane * 16. (The builtin exists only in the device
-// compilation pass; the host pass never executes device code.)
-__device__ __forceinline__ void glds16(const uint8_t* g, uint8_t* lds) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0);
-#endif
-}
-
-// Coalesced variant for a tile lying wholly inside the split. Per round the
-// wave fetches the next R bytes of all 64 lane chunks with
-// global_load_lds_dwordx4: instruction k brings the R-byte segments of lanes
-// k*SPI .. k*SPI+SPI-1 (whole 128-B lines) into LDS row k, the P = R/16 pieces
-// of segment q XOR-rotated by f(q) = (q / (16/P)) % P, which makes every
-// lane's ds_read_b128 of its piece j bank-conflict-free. One ring per wave:
-// the next round is issued as soon as the lane holds its pieces. After the
-// chunk, the lane finishes its last owned line with direct loads.
-template <int C, int R, class Step, int E>
-__device__ __forceinline__ uint32_t run_lane_staged(const ScanArgs& a, const Step& st, uint64_t cs, int lane,
-                                                    uint8_t* stage, LaneRun& r, const Emitter<E, false>& emit) {
-  constexpr int P = R / 16, SPI = 64 / P, G = 16 / P, NR = C / R;
-  static_assert(P * SPI == 64 && C % R == 0, "bad staging shape");
-  lane_init(a, cs, r);
-  const uint32_t M = a.start_m;
-  const uint8_t* tb = a.data + (cs - uint64_t(lane) * uint64_t(C));
-  uint32_t off[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const uint32_t q = uint32_t(k * SPI + lane / P);
-    off[k] = q * uint32_t(C) + 16u * (uint32_t(lane % P) ^ ((q / G) % P));
-  }
-  const uint8_t* rd = stage + (lane / SPI) * 1024 + 16 * ((lane % SPI) * P);
-  const int fl = (lane / G) % P;
-  constexpr bool kTrack = Step::kKind == kStepSheng8;
-  constexpr int D = DGREP_STAGE_DEPTH, RB = 64 * R;  // rounds in flight, bytes per round buffer
-  static_assert(D == 1 || D == 2, "stage depth 1 or 2");
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    if (d < NR) {
-#pragma unroll
-      for (int k = 0; k < P; ++k) glds16(tb + off[k] + uint32_t(d) * uint32_t(R), stage + d * RB + k * 1024);
-    }
-  }
-  for (int rr = 0; rr < NR; ++rr) {
-    // round rr has landed when only the P loads of round rr+1 (depth 2) may still be pending
-    if (D == 2 && rr + 1 < NR) {
-      if constexpr (P == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const int buf = D == 2 ? (rr & 1) : 0;
-    uint4 v[P];
-#pragma unroll
-    for (int j = 0; j < P; ++j) v[j] = *reinterpret_cast<const uint4*>(rd + buf * RB + 16 * (j ^ fl));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (rr + D < NR) {
-#pragma unroll
-      for (int k = 0; k < P; ++k)
-        glds16(tb + off[k] + uint32_t(rr + D) * uint32_t(R), stage + buf * RB + k * 1024);
-    }
-    run_block<R, kTrack>(st, M, v, uint64_t(rr) * R, uint64_t(C), r, emit);
-  }
-  const uint32_t nl_chunk = r.nl;
-  bool tail = true;
-  if constexpr (kTrack) {
-    // The last owned line ends at the right neighbour chunk's first '\n': the
-    // neighbour lane's transition map of that piece finishes it, so the chunk
-    // is not read again. (Lane 63's neighbour belongs to the next tile, and a
-    // neighbour chunk without '\n' means a longer line: those read on.)
-    const uint32_t nlo = __shfl_down(r.mlo, 1, 64), nhi = __shfl_down(r.mhi, 1, 64);
-    const int32_t np1 = __shfl_down(r.p1, 1, 64);
-    if (lane < 63 && np1 >= 0) {
-      tail = false;
-      if (r.seen && (__builtin_amdgcn_perm(nhi, nlo, r.s) & 0xffu) == M)
-        emit(r, uint64_t(C) + uint64_t(np1), r.prev_nl + 1, r.nl);
-    }
-  }
-  if (tail) run_lane_from<64>(a, st, cs, uint64_t(C), r, emit, uint32_t(C));
-  return nl_chunk;
-}
-
-// the coalesced staged path: small tables only (the staging ring and the
-// table share the CU's LDS)
-template <class Step, int TBL>
-constexpr bool use_staging() {
-  return (DGREP_SHENG_STAGING && Step::kKind == kStepSheng8) ||
-         (DGREP_TABLE_STAGING && Step::kKind == kStepTable && TBL <= 32 * int(kRow));
-}
-
 // The Sheng stepper's lane chunk is chosen per split on the host
 // (adaptive_chunk_bytes): the fixed chunks of the other steppers leave the
 // last round of tiles over the resident waves part-empty, which at 16-KiB
 // chunks costs up to a sixth of a 16-GiB split's time.
-// Only one-chunk-per-lane, unstaged steppers take the runtime chunk: the
-// two-chunk path (run_lane2) and the staged path are compiled for Tune::C.
+// Only one-chunk-per-lane steppers take the runtime chunk: the two-chunk path
+// (run_lane2) is compiled for Tune::C.
 template <class Step, int TBL>
 constexpr bool adaptive_chunk() {
   return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepFilter) &&
-         !use_staging<Step, TBL>() && streams_of<Step, TBL>() == 1;
+         streams_of<Step, TBL>() == 1;
 }
 template <class Step, int TBL>
 __device__ __forceinline__ uint32_t lane_chunk(const ScanArgs& a) {
@@ -1339,20 +901,11 @@ constexpr int waves_per_simd() {
 template <class Step, int TBL, int NT>
 __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(ScanArgs a) {
   constexpr int E = Tune<Step>::E, BK = Tune<Step>::B;
-  constexpr bool kStaged = use_staging<Step, TBL>();
   const uint32_t C = lane_chunk<Step, TBL>(a);
-  constexpr int R = DGREP_STAGE_ROUND;
   // per-lane slot stride: E slots per stream, plus the dummy of flat_emit
   constexpr int ES = E * streams_of<Step, TBL>() + (flat_emit<Step, false>() ? 1 : 0);
   static_assert(!flat_emit<Step, false>() || streams_of<Step, TBL>() == 1, "dummy slot: one stream per lane");
   __shared__ ScanSmem<TBL, ES, NT> sm;
-  // the staging rings are a __shared__ object of their own: with the table in
-  // the same object, hipcc cannot tell a ring write (global_load_lds) from a
-  // table read and drains vmcnt before every table lookup
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kStaged ? (NT / 64) * DGREP_STAGE_DEPTH * 64 * R : 16];
-  // the park (NT * BK bytes) keeps 3 workgroups per CU only beside tables up to 12 KiB
-  constexpr bool kDefer = use_defer<Step>() && !kStaged && TBL <= 12288;
-  __shared__ __attribute__((aligned(16))) uint8_t park[kDefer ? NT * BK : 16];
   const int tid = int(threadIdx.x);
   for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += NT * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
@@ -1385,17 +938,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         em.spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane;
         em.spill_cap = a.spill_per_lane;
       }
-      if constexpr (kStaged) {
-        if (full)
-          nlc[0] = run_lane_staged<Tune<Step>::C, R>(a, st, cs[0], lane, stage + (tid >> 6) * (DGREP_STAGE_DEPTH * 64 * R), r[0],
-                                         em);
-        else
-          nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
-      } else if constexpr (kDefer) {
-        nlc[0] = run_lane<BK, true>(a, st, cs[0], r[0], em, C, park + tid * BK, uint32_t(lane >> 1) & 7u);
-      } else {
-        nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
-      }
+      nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
     }
 
     // tile-wide exclusive scans of (newlines, matching lines) over the tile's
@@ -1867,10 +1410,7 @@ hipError_t overflow_t(const ScanArgs& a, uint64_t nover, hipStream_t stream) {
 template <class Step, int TBL>
 hipError_t occ_t(int* b) {
   constexpr int NT = threads_of<Step>();
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL, NT>, NT, 0);
-  // DGREP_MAX_WG_PER_CU (tuning, 0 = none): fewer resident lane streams per CU
-  if (DGREP_MAX_WG_PER_CU > 0 && *b > DGREP_MAX_WG_PER_CU) *b = DGREP_MAX_WG_PER_CU;
-  return e;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL, NT>, NT, 0);
 }
 
 // One switch for every entry point: stepper by kind, LDS image by size.
@@ -1879,7 +1419,7 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
   if (kind == kStepPair) {
     if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
-    if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB): 3 workgroups per CU with the park
+    if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB)
     if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
     return op.template run<StepPair, int(kPairMaxImage)>();
   }

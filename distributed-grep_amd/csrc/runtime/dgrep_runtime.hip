@@ -208,9 +208,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   const uint32_t Sp = S + uint32_t(targets.size());
   // bytes per T2 row: 2K^2, padded to an ODD number of dwords so that the
   // same column of different rows falls in different LDS banks
-  uint64_t row = 2ull * K * K;
-  if (DGREP_PAIR_ROWPAD) row = ((row + 3) & ~3ull) | 4ull;
-  if (row * Sp > kPairMaxT2 || (DGREP_PAIR_U8 && 2 * (K - 1) > 255)) return false;
+  const uint64_t row = ((2ull * K * K + 3) & ~3ull) | 4ull;
+  if (row * Sp > kPairMaxT2) return false;
   const uint64_t t1_off = (kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
   if (end > kPairMaxImage) return false;
   std::vector<uint32_t> id(S), orig(Sp);
@@ -245,12 +244,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   }
   for (int b = 0; b < 256; ++b) {
     const uint32_t c = h.byte_class[b];
-    if (DGREP_PAIR_U8) {
-      img->data()[b] = uint8_t(2u * c);  // CL[b]
-    } else {
-      ua[pair_swz(uint32_t(b))] = 2u * K * c;
-      ub[pair_swz(uint32_t(b))] = 2u * c;
-    }
+    ua[b] = 2u * K * c;
+    ub[b] = 2u * c;
   }
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
@@ -299,10 +294,7 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
   const uint32_t Sf = next;
   auto to = [&](uint32_t x) { return uint16_t((id[x] == UINT32_MAX ? CAND : id[x]) * K); };
   img->assign((kFilterClassBytes + size_t(Sf) * K * 2 + 15) & ~size_t(15), 0);
-  for (int b = 0; b < 256; ++b) {
-    if (DGREP_FILTER_CLS32) reinterpret_cast<uint32_t*>(img->data())[b] = h.byte_class[b];
-    else img->data()[b] = h.byte_class[b];
-  }
+  for (int b = 0; b < 256; ++b) img->data()[b] = h.byte_class[b];
   uint16_t* rows = reinterpret_cast<uint16_t*>(img->data() + kFilterClassBytes);
   for (uint32_t i = 0; i < keep; ++i) {
     const uint32_t x = order[i];
@@ -559,7 +551,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     t.assign(256 * 8, 0);
     for (int b = 0; b < 256; ++b)
       for (uint32_t s = 0; s < S; ++s)
-        t[size_t(sheng_swz(uint32_t(b))) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
+        t[size_t(b) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
     start = id[h.start] * 0x01010101u;
     start_m = top;
   } else {

@@ -1,10 +1,10 @@
 #!/bin/bash
-# A/B the tuning variants built by `make -C distributed-grep_amd variants` (run ON the GPU box).
+# A/B the tuning variants built by tools/build_variants.sh (run ON the GPU box).
 #   tools/variant_bench.sh <workload> [variant ...]
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 WL=${1:-c2}; shift || true
-VARS=${@:-base sw3 sc2k sr64 tw4}
+VARS=${@:-base}
 for v in $VARS; do
   for rep in $(seq ${REPS:-2}); do
     out=$(DGREP_LIB=$R/distributed-grep_amd/variants/libdgrep_$v.so timeout -k 10 180 python3 $R/bench.py --workload $WL --steps 6 --warmup 2 --no-cpu-baseline --verify-windows 3 2>/dev/null) || { echo "$v FAILED"; exit 1; }
