@@ -13,9 +13,20 @@
 // Build (in the reference tree, next to application/grep.go):
 //   go build -buildmode=plugin -o grep.so ./application
 // with this repository's include/ and distributed-grep_amd/libdgrep.so on the
-// cgo paths below. There is no Go toolchain in this image or on the GPU box;
-// tests/abi_c/plugin_sequence.c runs the same call sequence from C and is
-// tested on the GPU (tests/test_abi_c.py).
+// cgo paths below. UNTESTED AS GO: there is no Go toolchain in this image or
+// on the GPU box; tests/abi_c/plugin_sequence.c runs the same call sequence
+// from C and is tested on the GPU (tests/test_abi_c.py).
+//
+// Intended departures from grep.go (fail-stop, never a silent CPU path): a
+// valid Go pattern outside the compiler's subset (DGREP_E_UNSUPPORTED /
+// DGREP_E_TOO_LARGE) panics at the first Map, as does any HIP error; the
+// worker dies and the coordinator's 10 s timeout re-assigns the task
+// (map_reduce/coordinator.go:97-124). A pattern Go itself rejects is not a
+// departure: it compiles to a match-nothing blob, as grep.go:21 drops the error.
+//
+// Device: dgrep_pick_device(-1) -- DGREP_DEVICE, else DGREP_WORKER_ID (or the
+// process id) modulo the device count, so N worker processes on one node
+// spread over its GPUs (the plugin never sees the RPC's WorkerID).
 package main
 
 /*
@@ -62,7 +73,11 @@ func setup() {
 		panic("dgrep_compile: " + C.GoString(&errbuf[0])) // unsupported construct: refuse, never guess
 	}
 	defer C.dgrep_blob_free(blob)
-	if rc := C.dgrep_open(0, &ctx); rc != C.DGREP_OK {
+	var dev C.int
+	if rc := C.dgrep_pick_device(-1, &dev); rc != C.DGREP_OK {
+		panic(fmt.Sprintf("dgrep_pick_device: rc=%d (DGREP_DEVICE=%q)", int(rc), os.Getenv("DGREP_DEVICE")))
+	}
+	if rc := C.dgrep_open(dev, &ctx); rc != C.DGREP_OK {
 		panic("dgrep_open: " + C.GoString(C.dgrep_last_error(ctx)))
 	}
 	if rc := C.dgrep_load_dfa(ctx, blob, n); rc != C.DGREP_OK {
@@ -75,6 +90,7 @@ func Map(filename string, contents string) []mapreduce.KeyValue {
 	once.Do(setup)
 	runtime.LockOSThread()
 	defer runtime.UnlockOSThread()
+	// Go 1.18 (go.mod:3) has no unsafe.StringData (1.20): the string header
 	hdr := (*reflect.StringHeader)(unsafe.Pointer(&contents))
 	var res C.dgrep_result
 	// contents holds no Go pointers, so passing its bytes obeys the cgo rules;
@@ -88,9 +104,9 @@ func Map(filename string, contents string) []mapreduce.KeyValue {
 	if n == 0 {
 		return kva
 	}
-	lines := (*[1 << 40]C.uint64_t)(unsafe.Pointer(res.line_no))[:n:n]
-	starts := (*[1 << 40]C.uint64_t)(unsafe.Pointer(res.start))[:n:n]
-	lens := (*[1 << 40]C.uint32_t)(unsafe.Pointer(res.len))[:n:n]
+	lines := unsafe.Slice(res.line_no, n) // unsafe.Slice: Go 1.17+
+	starts := unsafe.Slice(res.start, n)
+	lens := unsafe.Slice(res.len, n)
 	for i := 0; i < n; i++ {
 		s := int(starts[i])
 		k := fmt.Sprintf("%s (line number #%v)", filename, uint64(lines[i]))

@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 STAGED_LINE_BYTES = 16  # StagedLine written by the scan kernel per match
+LEN_DTYPE = "int32"  # torch dtype of the length array dgrep_scan_device writes (uint32 in dgrep.h)
 
 WORKLOADS = {
     # BASELINE.json configs[0] / SURVEY §8d C1: the reference's CPU-runnable case
@@ -83,6 +84,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="CPU baseline budget: whole 1 MiB pieces of the split until this much time is spent")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", choices=["full", "windows", "none"], default="full",
+                    help="after the timed steps: every record of the split against the oracle over the whole split "
+                         "(full; each rank its own split), or --verify-windows whole-line windows")
+    ap.add_argument("--verify-seconds", type=float, default=240.0,
+                    help="full verification stops (and says how far it got) after this much wall time")
     ap.add_argument("--verify-windows", type=int, default=6)
     ap.add_argument("--lane-chunk", type=int, default=0, help="tuning: force the Sheng/pair/filter lane chunk (0 = adaptive)")
     ap.add_argument("--pattern", default=None,
@@ -176,7 +182,7 @@ def main():
     res = None
     for _ in range(3):
         res = (torch.empty(cap, dtype=torch.int64, device=dev), torch.empty(cap, dtype=torch.int64, device=dev),
-               torch.empty(cap, dtype=torch.int32, device=dev))
+               torch.empty(cap, dtype=getattr(torch, LEN_DTYPE), device=dev))
         cnt = ctx.scan_device(buf.data_ptr(), n, res[0].data_ptr(), res[1].data_ptr(), res[2].data_ptr(), cap)
         if cnt <= cap:
             break
@@ -189,7 +195,7 @@ def main():
         c = ctx.scan_device(buf.data_ptr(), n, line_t.data_ptr(), start_t.data_ptr(), len_t.data_ptr(), cap)
         if world > 1:
             # the path's only exchange: compacted records -> rank 0 over RCCL/xGMI
-            gather_records(line_t, start_t, len_t, c, dst=0)
+            gather_records(line_t, start_t, len_t, c, dst=0, split=seed)
         return c
 
     for _ in range(args.warmup):
@@ -219,11 +225,20 @@ def main():
     st = stats[-1]
     achieved = (n + STAGED_LINE_BYTES * count) / (kern_ms * 1e-3) / 1e9
 
-    # ---- size-independent checks on the full split (rank 0) ----------------
+    # ---- parity on the full split: every rank checks its own ----------------
     verified = None
-    if rank == 0 and args.verify_windows > 0:
-        verified = verify_windows(buf, n, line_t[:count], start_t[:count], len_t[:count], pattern,
-                                  args.verify_windows, wl.get("verify_window", 2 << 20))
+    if args.verify == "full":
+        threads = verify_threads(world)
+        verified = verify_full(buf, n, line_t[:count], start_t[:count], len_t[:count], pattern, threads,
+                               args.verify_seconds)
+        if world > 1:
+            ok = torch.tensor([verified["records_checked"], int(verified["complete"])], dtype=torch.int64, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            verified["all_ranks_complete"] = bool(ok[1].item())
+    elif args.verify == "windows" and rank == 0 and args.verify_windows > 0:
+        verified = {"mode": "windows", "windows": verify_windows(buf, n, line_t[:count], start_t[:count],
+                                                                 len_t[:count], pattern, args.verify_windows,
+                                                                 wl.get("verify_window", 2 << 20))}
 
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -267,7 +282,7 @@ def main():
                 "parallelism": "1 split per GPU x %d" % world,
                 "per_gpu_gbs": round(value / world, 2),
                 "hbm_frac_whole_node": round(value / (HBM_PEAK_GBS * world), 4),
-                "verified_windows": verified,
+                "verified": verified,
                 "seed": seed,
                 "stepper": st["stepper"],
                 "lane_chunk": st["lane_chunk"],
@@ -300,6 +315,82 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def last_newline(host):
+    """Index of the last '\n' in a host uint8 array (-1: none), searching the
+    tail first."""
+    import numpy as np
+
+    span = 1 << 20
+    end = len(host)
+    while end > 0:
+        lo = max(0, end - span)
+        nl = np.flatnonzero(host[lo:end] == 10)
+        if nl.size:
+            return lo + int(nl[-1])
+        end = lo
+        span *= 4
+    return -1
+
+
+def verify_threads(world):
+    """Host threads for the oracle: the process's CPU share split over the ranks
+    of this node, 16 at most (the GPU box grants 16 CPUs per GPU)."""
+    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(16, cpus // max(1, world)))
+
+
+def verify_full(buf, n, line_t, start_t, len_t, pattern, threads, seconds, piece=1 << 30):
+    """Parity at full size: the oracle's Map (orc_map_mt, the memoized Pike VM
+    restatement of grep.go:17-29) over the WHOLE split, in ~1 GiB pieces cut
+    after a '\n', must equal every GPU record -- line number (offset by the
+    '\n' count before the piece), start and length. Also the structural check
+    of every record (check_records). Stops after `seconds` of wall time and
+    reports how far it got (`complete` false)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    t0 = time.time()
+    check_records(buf, n, line_t, start_t, len_t)
+    gl = line_t.cpu().numpy().astype(np.uint64)
+    gs = start_t.cpu().numpy().astype(np.uint64)
+    ge = len_t.cpu().numpy().astype(np.uint64)
+    a, lines_before, checked, pieces = 0, 0, 0, 0
+    while a < n:
+        if time.time() - t0 > seconds:
+            break
+        host = buf[a:min(n, a + piece)].cpu().numpy()
+        last = a + len(host) >= n
+        if not last:
+            cut = last_newline(host)
+            if cut < 0:  # no '\n' in the whole piece (a line over 1 GiB): take the rest of the split
+                host = buf[a:n].cpu().numpy()
+                last = True
+            else:
+                host = host[:cut + 1]
+        b = a + len(host)
+        ln, st, le = O.grep_map(pattern.encode(), memoryview(host), threads=threads)
+        if not last and len(st) and int(st[-1]) == len(host):
+            ln, st, le = ln[:-1], st[:-1], le[:-1]  # the empty piece after the cut's '\n' is not a line
+        i, j = np.searchsorted(gs, a), np.searchsorted(gs, b if not last else n + 1)
+        np.testing.assert_array_equal(gl[i:j], ln.astype(np.uint64) + np.uint64(lines_before),
+                                      err_msg="line numbers in piece at %d" % a)
+        np.testing.assert_array_equal(gs[i:j], st.astype(np.uint64) + np.uint64(a), err_msg="starts at %d" % a)
+        np.testing.assert_array_equal(ge[i:j], le.astype(np.uint64), err_msg="lengths at %d" % a)
+        lines_before += int(np.count_nonzero(host == 10))
+        checked += j - i
+        pieces += 1
+        a = b
+    complete = a >= n and checked == len(gs)
+    log("full-split parity: %s records equal the oracle over %.2f GiB (%d pieces, %d threads, %.1f s)%s" % (
+        checked, a / 2**30, pieces, threads, time.time() - t0, "" if complete else " -- INCOMPLETE (time budget)"))
+    if complete:
+        log("all %d records equal the oracle" % checked)
+    return {"mode": "full", "complete": bool(complete), "records_checked": int(checked), "bytes_checked": int(a),
+            "oracle_threads": threads, "seconds": round(time.time() - t0, 1)}
 
 
 def verify_windows(buf, n, line_t, start_t, len_t, pattern, k, win):

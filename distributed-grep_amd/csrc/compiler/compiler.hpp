@@ -19,7 +19,7 @@ struct CompiledDfa {
 };
 
 // AST -> minimal line-matching DFA (see dfa_builder.cpp). DGREP_OK or DGREP_E_TOO_LARGE.
-int build_dfa(const Re& re, CompiledDfa* out, std::string* err);
+int build_dfa(const Re& re, CompiledDfa* out, std::string* err, size_t state_budget = 0);
 // The automaton of a pattern that matches no line.
 void dfa_match_none(CompiledDfa* out, uint32_t extra_flags);
 

@@ -706,7 +706,9 @@ bool DfaBuilder::run(CompiledDfa* out, CompiledDfa* partial, size_t budget) {
 }  // namespace
 
 // Builds the DFA for a parsed pattern. Returns DGREP_OK / DGREP_E_TOO_LARGE.
-int build_dfa(const Re& re, CompiledDfa* out, std::string* err) {
+// state_budget (0 = kMaxDfaStates; tests pass a small one so that the partial
+// DFA + NFA program path is checked on small patterns, dgrep_compile_budget).
+int build_dfa(const Re& re, CompiledDfa* out, std::string* err, size_t state_budget) {
   NfaBuilder nfa;
   Frag f = nfa.build(re);
   int32_t m = nfa.add(NState{NState::Match});
@@ -717,13 +719,7 @@ int build_dfa(const Re& re, CompiledDfa* out, std::string* err) {
   Decoder dec;
   dec.build(rc);
   DfaBuilder b(nfa, f.start, rc, dec);
-  // DGREP_DFA_STATE_BUDGET (tests only) lowers the budget so that the partial
-  // DFA + NFA program path can be checked on small patterns
-  size_t budget = kMaxDfaStates;
-  if (const char* e = getenv("DGREP_DFA_STATE_BUDGET")) {
-    const long v = strtol(e, nullptr, 10);
-    if (v >= 3 && size_t(v) < budget) budget = size_t(v);
-  }
+  const size_t budget = state_budget >= 3 && state_budget < kMaxDfaStates ? state_budget : kMaxDfaStates;
   CompiledDfa part;
   if (b.run(out, &part, budget)) return DGREP_OK;
   // over the DFA budget: the first states as a filter, the NFA program decides

@@ -15,6 +15,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../../include/dgrep.h"
 #include "../../../include/dgrep_blob.h"
 #include "../kernels/encode.h"
@@ -313,6 +315,31 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
 }
 
 }  // namespace
+
+extern "C" int dgrep_pick_device(int worker_id, int* device) {
+  if (!device) return DGREP_E_INVALID;
+  *device = -1;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return DGREP_E_HIP;
+  long dev;
+  if (const char* e = getenv("DGREP_DEVICE")) {
+    char* end = nullptr;
+    dev = strtol(e, &end, 10);
+    if (!*e || *end || dev < 0) return DGREP_E_INVALID;
+    if (dev >= count) return DGREP_E_HIP;
+  } else {
+    long id = worker_id;
+    if (id < 0) {
+      const char* w = getenv("DGREP_WORKER_ID");
+      char* end = nullptr;
+      id = w && *w ? strtol(w, &end, 10) : -1;
+      if (id < 0 || (end && *end)) id = long(getpid());
+    }
+    dev = id % count;
+  }
+  *device = int(dev);
+  return DGREP_OK;
+}
 
 extern "C" int dgrep_open(int device, dgrep_ctx** out) {
   if (!out) return DGREP_E_INVALID;

@@ -49,8 +49,8 @@ DFA_PARTIAL = 8
 
 # Symbols declared in include/dgrep.h (tests check the library exports all).
 EXPORTS = (
-    "dgrep_compile", "dgrep_blob_free", "dgrep_blob_info_get", "dgrep_open", "dgrep_close",
-    "dgrep_last_error", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
+    "dgrep_compile", "dgrep_compile_budget", "dgrep_blob_free", "dgrep_blob_info_get", "dgrep_open", "dgrep_close",
+    "dgrep_last_error", "dgrep_pick_device", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
     "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_lane_chunk", "dgrep_set_ingest", "dgrep_last_ingest_ms",
     "dgrep_map_partitions", "dgrep_partitions_free", "dgrep_encode_device", "dgrep_last_encode_ms",
@@ -113,10 +113,15 @@ def lib() -> ctypes.CDLL:
             vp, sz, u64, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
             L.dgrep_compile.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.c_char_p, sz]
             L.dgrep_compile.restype = i
+            L.dgrep_compile_budget.argtypes = [ctypes.c_char_p, sz, ctypes.c_uint32, ctypes.POINTER(vp),
+                                               ctypes.POINTER(sz), ctypes.c_char_p, sz]
+            L.dgrep_compile_budget.restype = i
             L.dgrep_blob_free.argtypes = [vp]
             L.dgrep_blob_free.restype = None
             L.dgrep_blob_info_get.argtypes = [vp, sz, ctypes.POINTER(_BlobInfo)]
             L.dgrep_blob_info_get.restype = i
+            L.dgrep_pick_device.argtypes = [i, ctypes.POINTER(i)]
+            L.dgrep_pick_device.restype = i
             L.dgrep_open.argtypes = [i, ctypes.POINTER(vp)]
             L.dgrep_open.restype = i
             L.dgrep_close.argtypes = [vp]
@@ -174,7 +179,9 @@ def lib() -> ctypes.CDLL:
 class CompiledPattern:
     """A pattern compiled by dgrep_compile (Go regexp/syntax semantics)."""
 
-    def __init__(self, pattern):
+    def __init__(self, pattern, state_budget: int = 0):
+        """state_budget (tests only): a lowered DFA state budget, so that small
+        patterns compile to partial blobs (dgrep_compile_budget)."""
         if isinstance(pattern, str):
             pattern = pattern.encode("utf-8", "surrogateescape")
         self.pattern = bytes(pattern)
@@ -182,7 +189,8 @@ class CompiledPattern:
         blob = ctypes.c_void_p()
         n = ctypes.c_size_t()
         err = ctypes.create_string_buffer(512)
-        rc = L.dgrep_compile(self.pattern, len(self.pattern), ctypes.byref(blob), ctypes.byref(n), err, 512)
+        rc = L.dgrep_compile_budget(self.pattern, len(self.pattern), state_budget, ctypes.byref(blob),
+                                    ctypes.byref(n), err, 512)
         msg = err.value.decode(errors="replace")
         if rc == DGREP_E_UNSUPPORTED:
             raise UnsupportedPattern(rc, msg)
@@ -418,10 +426,20 @@ def set_pattern(p: str):
     pattern = p
 
 
+def pick_device(worker_id: int = -1) -> int:
+    """dgrep_pick_device: DGREP_DEVICE, else worker_id % device count (worker_id
+    < 0: DGREP_WORKER_ID, else the process id). Raises if the device is absent."""
+    d = ctypes.c_int()
+    rc = lib().dgrep_pick_device(worker_id, ctypes.byref(d))
+    if rc != DGREP_OK:
+        raise DgrepError(rc, "no such device (DGREP_DEVICE=%r, worker %d)" % (os.environ.get("DGREP_DEVICE"), worker_id))
+    return d.value
+
+
 def _context() -> Context:
     ctx = getattr(_ctx_local, "ctx", None)
     if ctx is None:
-        ctx = Context(int(os.environ.get("DGREP_DEVICE", "0")))
+        ctx = Context(pick_device())
         _ctx_local.ctx = ctx
         _ctx_local.loaded = None
     if _ctx_local.loaded != pattern:

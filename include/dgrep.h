@@ -81,10 +81,28 @@ typedef struct {
  * the reference discards the error and matches nothing. `err` (optional)
  * receives a message for non-OK results. */
 int dgrep_compile(const char* pattern, size_t n, void** blob, size_t* blob_len, char* err, size_t errlen);
+/* Tests only: dgrep_compile with the DFA state budget lowered to state_budget
+ * (0 = the default 2^21; values below 3 are ignored), so that the partial-blob
+ * path (DGREP_DFA_PARTIAL) can be exercised with small patterns. */
+int dgrep_compile_budget(const char* pattern, size_t n, uint32_t state_budget, void** blob, size_t* blob_len,
+                         char* err, size_t errlen);
 void dgrep_blob_free(void* blob);
+/* Validates the whole blob (header, byte classes, every transition, and the
+ * NFA program of a partial blob word by word) before reporting its header:
+ * DGREP_E_INVALID if anything would index out of range. dgrep_load_dfa
+ * calls it first. */
 int dgrep_blob_info_get(const void* blob, size_t n, dgrep_blob_info* info);
 
 /* ---- device context ------------------------------------------------------ */
+/* The worker's device (map_reduce/worker.go:126-145 runs one map task at a
+ * time per worker process, one file per task, coordinator.go:312,329-333): the
+ * DGREP_DEVICE environment variable if set, else worker_id % device_count, where
+ * a negative worker_id means the DGREP_WORKER_ID environment variable, else the
+ * process id (the Go plugin has no worker id: WorkerID stays inside the RPC
+ * reply, worker.go:144). A device that is not present -- DGREP_DEVICE=99 on an
+ * 8-GPU node, or no GPU at all -- is DGREP_E_HIP; a DGREP_DEVICE that is not a
+ * non-negative integer is DGREP_E_INVALID. */
+int dgrep_pick_device(int worker_id, int* device);
 int dgrep_open(int device, dgrep_ctx** ctx);
 void dgrep_close(dgrep_ctx* ctx);
 const char* dgrep_last_error(dgrep_ctx* ctx);

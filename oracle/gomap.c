@@ -67,13 +67,14 @@ typedef struct {
 
 static void* slice_run(void* arg) {
   Slice* s = (Slice*)arg;
+  orc_matcher* mt = orc_matcher_new(s->re);
   size_t ls = s->lo;
   uint64_t ln = s->first_line;
   s->cnt = 0;
   while (ls < s->hi || (s->last && ls == s->hi)) {
     const unsigned char* nl = ls < s->hi ? memchr(s->c + ls, '\n', s->hi - ls) : NULL;
     size_t le = nl ? (size_t)(nl - s->c) : s->hi;
-    if (orc_match(s->re, s->c + ls, le - ls)) {
+    if (orc_matcher_match(mt, s->c + ls, le - ls)) {
       if (s->cnt >= s->cap) {
         s->cap = s->cap ? s->cap * 2 : 1024;
         s->ln = realloc(s->ln, s->cap * sizeof(uint64_t));
@@ -87,6 +88,7 @@ static void* slice_run(void* arg) {
     if (!nl) break;
     ls = le + 1;
   }
+  orc_matcher_free(mt);
   return NULL;
 }
 

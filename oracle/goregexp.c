@@ -1045,3 +1045,160 @@ int orc_match(const orc_re* pg, const unsigned char* s, size_t n) {
   free(mem);
   return matched;
 }
+
+/* ---- memoized Pike VM: a lazy DFA over the same program -------------------
+ * For whole-split checks (orc_map_mt). A state is what orc_match carries from
+ * one rune to the next: the set of pcs reached by the last rune step (`raw`,
+ * kept sorted) and the class of the previous rune -- the only part of it that
+ * empty_ctx() reads: none yet (-1), an ASCII word character, '\n', or other.
+ * The transition of a state on a rune, and its verdict at the end of the line,
+ * are computed by exactly the closure/step code of orc_match and cached for
+ * ASCII runes; other runes are computed every time. The cache is flushed when
+ * it grows past its bounds. */
+enum { PC_BOT = 0, PC_WORD = 1, PC_NL = 2, PC_OTHER = 3 };
+static const int pc_rep[4] = {-1, 'a', '\n', ' '};
+static int prev_class(int r) { return r < 0 ? PC_BOT : is_word(r) ? PC_WORD : r == '\n' ? PC_NL : PC_OTHER; }
+
+#define LZ_MATCHED (-2)
+#define LZ_UNKNOWN (-1)
+#define LZ_MAX_STATES 8192
+#define LZ_MAX_ARENA (1 << 22)
+
+typedef struct {
+  int set_off, nset, prev;
+  int endm; /* -1 unknown, else the end-of-line verdict */
+  int next[128];
+} LzState;
+
+struct orc_matcher {
+  const orc_re* pg;
+  LzState* st; int nst;
+  int* arena; int narena;
+  int* hash; int hcap; /* open addressing: state index + 1, 0 = empty */
+  SSet cur, nxt;
+  int* mem; int* stack; int* raw;
+  int start_state;
+};
+
+static uint64_t lz_hash(const int* s, int n, int prev) {
+  uint64_t h = 1469598103934665603ull ^ (uint64_t)prev;
+  for (int i = 0; i < n; i++) { h ^= (uint64_t)(unsigned)s[i]; h *= 1099511628211ull; }
+  return h ^ (h >> 29);
+}
+
+static int cmp_int(const void* a, const void* b) { int x = *(const int*)a, y = *(const int*)b; return (x > y) - (x < y); }
+
+static void lz_reset(orc_matcher* m) {
+  m->nst = 0;
+  m->narena = 0;
+  memset(m->hash, 0, sizeof(int) * (size_t)m->hcap);
+}
+
+/* intern (sorted set, prev); returns the state index */
+static int lz_intern(orc_matcher* m, const int* s, int n, int prev) {
+  uint64_t h = lz_hash(s, n, prev);
+  for (uint64_t i = h & (uint64_t)(m->hcap - 1);; i = (i + 1) & (uint64_t)(m->hcap - 1)) {
+    int e = m->hash[i];
+    if (!e) {
+      LzState* x = &m->st[m->nst];
+      x->set_off = m->narena; x->nset = n; x->prev = prev; x->endm = LZ_UNKNOWN;
+      for (int k = 0; k < 128; k++) x->next[k] = LZ_UNKNOWN;
+      memcpy(m->arena + m->narena, s, sizeof(int) * (size_t)n);
+      m->narena += n;
+      m->hash[i] = ++m->nst;
+      return m->nst - 1;
+    }
+    const LzState* x = &m->st[e - 1];
+    if (x->prev == prev && x->nset == n && !memcmp(m->arena + x->set_off, s, sizeof(int) * (size_t)n)) return e - 1;
+  }
+}
+
+/* closure of the state's set and of the start under ctx(prev, r): 1 = Match */
+static int lz_closure(orc_matcher* m, const int* set, int n, int prev, int r) {
+  const int ctx = empty_ctx(pc_rep[prev], r);
+  m->cur.n = 0;
+  int matched = 0;
+  for (int i = 0; i < n && !matched; i++) matched = closure(m->pg, &m->cur, set[i], ctx, m->stack);
+  if (!matched) matched = closure(m->pg, &m->cur, m->pg->start, ctx, m->stack);
+  return matched;
+}
+
+/* the transition of state `si` on rune r >= 0 (LZ_MATCHED or a state index);
+ * *sip is updated if the cache had to be flushed */
+static int lz_step(orc_matcher* m, int* sip, int r) {
+  LzState* x = &m->st[*sip];
+  int n = x->nset, prev = x->prev;
+  /* the set may move if the cache is flushed below: work on a copy */
+  memcpy(m->raw, m->arena + x->set_off, sizeof(int) * (size_t)n);
+  if (lz_closure(m, m->raw, n, prev, r)) return LZ_MATCHED;
+  int nraw = 0;
+  m->nxt.n = 0;
+  for (int i = 0; i < m->cur.n; i++) {
+    const Inst* in = &m->pg->in[m->cur.dense[i]];
+    if (in->op >= I_RUNE && rune_match(in, r) && in->out >= 0 && !ss_has(&m->nxt, in->out)) {
+      ss_add(&m->nxt, in->out);
+      m->raw[nraw++] = in->out;
+    }
+  }
+  qsort(m->raw, (size_t)nraw, sizeof(int), cmp_int);
+  if (m->nst + 2 > LZ_MAX_STATES || m->narena + nraw + m->pg->n > LZ_MAX_ARENA) {
+    /* flush: re-intern the current state first so the caller's index stays valid */
+    int* keep = (int*)malloc(sizeof(int) * ((size_t)n + 1));
+    memcpy(keep, m->arena + m->st[*sip].set_off, sizeof(int) * (size_t)n);
+    lz_reset(m);
+    m->start_state = lz_intern(m, NULL, 0, PC_BOT);
+    *sip = lz_intern(m, keep, n, prev);
+    free(keep);
+  }
+  return lz_intern(m, m->raw, nraw, prev_class(r));
+}
+
+orc_matcher* orc_matcher_new(const orc_re* pg) {
+  orc_matcher* m = (orc_matcher*)calloc(1, sizeof(orc_matcher));
+  m->pg = pg;
+  if (pg->status != ORC_OK) return m;
+  int N = pg->n;
+  m->st = (LzState*)malloc(sizeof(LzState) * LZ_MAX_STATES);
+  m->arena = (int*)malloc(sizeof(int) * (size_t)LZ_MAX_ARENA);
+  m->hcap = 4 * LZ_MAX_STATES;
+  m->hash = (int*)calloc((size_t)m->hcap, sizeof(int));
+  m->mem = (int*)malloc(sizeof(int) * ((size_t)N * 6 + 16));
+  m->cur = (SSet){m->mem, m->mem + N, 0};
+  m->nxt = (SSet){m->mem + 2 * N, m->mem + 3 * N, 0};
+  m->stack = m->mem + 4 * N;
+  m->raw = (int*)malloc(sizeof(int) * ((size_t)N + 4));
+  m->start_state = lz_intern(m, NULL, 0, PC_BOT);
+  return m;
+}
+
+int orc_matcher_match(orc_matcher* m, const unsigned char* s, size_t n) {
+  if (m->pg->status != ORC_OK) return 0;
+  int si = m->start_state;
+  size_t pos = 0;
+  while (pos < n) {
+    int r, sz;
+    if (s[pos] < 0x80) { r = s[pos]; sz = 1; } else r = dec_rune(s + pos, n - pos, &sz);
+    int nx = r < 128 ? m->st[si].next[r] : LZ_UNKNOWN;
+    if (nx == LZ_UNKNOWN) {
+      int cur = si;
+      nx = lz_step(m, &cur, r);
+      if (nx != LZ_MATCHED && r < 128) m->st[cur].next[r] = nx;
+      else if (nx == LZ_MATCHED && r < 128) m->st[cur].next[r] = LZ_MATCHED;
+    }
+    if (nx == LZ_MATCHED) return 1;
+    si = nx;
+    pos += (size_t)sz;
+  }
+  LzState* x = &m->st[si];
+  if (x->endm == LZ_UNKNOWN) {
+    memcpy(m->raw, m->arena + x->set_off, sizeof(int) * (size_t)x->nset);
+    x->endm = lz_closure(m, m->raw, x->nset, x->prev, -1);
+  }
+  return x->endm;
+}
+
+void orc_matcher_free(orc_matcher* m) {
+  if (!m) return;
+  free(m->st); free(m->arena); free(m->hash); free(m->mem); free(m->raw);
+  free(m);
+}

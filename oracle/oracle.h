@@ -42,6 +42,13 @@ int orc_compile(const char* pat, size_t n, orc_re** out, char* err, size_t errle
 /* regexp.Match semantics on one line: unanchored, boolean. */
 int orc_match(const orc_re* re, const unsigned char* s, size_t n);
 void orc_free(orc_re* re);
+/* The same verdicts as orc_match, memoized: a lazy DFA whose states are
+ * orc_match's own (pc set, previous-rune class) pairs, built on demand (one
+ * matcher per thread). Used by orc_map_mt for whole-split checks. */
+typedef struct orc_matcher orc_matcher;
+orc_matcher* orc_matcher_new(const orc_re* re);
+int orc_matcher_match(orc_matcher* m, const unsigned char* s, size_t n);
+void orc_matcher_free(orc_matcher* m);
 
 /*
  * grep.go Map restatement: split `contents` on '\n' (strings.Split: k newlines

@@ -11,8 +11,8 @@
  * main/worker_launch.go:16-18 -> map_reduce/worker.go:126-145).
  *
  * Usage: plugin_sequence <pattern-file> <split-file> <out-file>
- * Writes the records of the main-thread scan, then those of the pthread scan,
- * as "line_no start len" lines, each block preceded by "# <count>". Exit 0 on
+ * Writes the records of the main-thread scan, the pthread scan and a second
+ * context's scan on the same device, as "line_no start len" lines, each block preceded by "# <count>". Exit 0 on
  * success; tests/test_abi_c.py compares the output with the oracle.
  */
 #include <pthread.h>
@@ -84,9 +84,18 @@ int main(int argc, char** argv) {
   dgrep_blob_info info;
   CHECK(dgrep_blob_info_get(blob, blen, &info) == DGREP_OK, "blob info");
 
+  /* the worker's device: DGREP_DEVICE, else worker id % device count */
+  int dev = -1;
+  rc = dgrep_pick_device(-1, &dev);
+  CHECK(rc == DGREP_OK, "dgrep_pick_device rc=%d (DGREP_DEVICE=%s)", rc,
+        getenv("DGREP_DEVICE") ? getenv("DGREP_DEVICE") : "unset");
   dgrep_ctx* ctx = NULL;
-  rc = dgrep_open(0, &ctx);
+  rc = dgrep_open(dev, &ctx);
   CHECK(rc == DGREP_OK, "dgrep_open rc=%d: %s", rc, ctx ? dgrep_last_error(ctx) : "");
+  /* a second context on the same device (one per stream; no shared state) */
+  dgrep_ctx* ctx2 = NULL;
+  rc = dgrep_open(dev, &ctx2);
+  CHECK(rc == DGREP_OK, "second dgrep_open rc=%d", rc);
 
   /* a scan before any pattern: DGREP_E_NO_DFA with a message */
   dgrep_result r0;
@@ -101,6 +110,8 @@ int main(int argc, char** argv) {
 
   rc = dgrep_load_dfa(ctx, blob, blen);
   CHECK(rc == DGREP_OK, "dgrep_load_dfa rc=%d: %s", rc, dgrep_last_error(ctx));
+  rc = dgrep_load_dfa(ctx2, blob, blen);
+  CHECK(rc == DGREP_OK, "second dgrep_load_dfa rc=%d: %s", rc, dgrep_last_error(ctx2));
   dgrep_blob_free(blob);
 
   FILE* out = fopen(argv[3], "w");
@@ -122,6 +133,14 @@ int main(int argc, char** argv) {
   CHECK(j.rc == DGREP_OK, "pthread dgrep_scan rc=%d: %s", j.rc, dgrep_last_error(ctx));
   dump(out, &j.res);
   dgrep_result_free(&j.res);
+
+  /* the second context scans the same split independently */
+  dgrep_result r2;
+  rc = dgrep_scan(ctx2, data, n, &r2);
+  CHECK(rc == DGREP_OK, "second context dgrep_scan rc=%d: %s", rc, dgrep_last_error(ctx2));
+  dump(out, &r2);
+  dgrep_result_free(&r2);
+  dgrep_close(ctx2);
 
   fclose(out);
   dgrep_close(ctx);

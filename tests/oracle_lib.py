@@ -84,7 +84,8 @@ def grep_map(pattern: bytes, contents: bytes, recompile_per_line=False, threads=
     buf = np.frombuffer(contents, dtype=np.uint8) if len(contents) else np.zeros(1, np.uint8)
     ptr = buf.ctypes.data
     L = lib()
-    cap = 0
+    # at most one record per line: one pass fills the arrays
+    cap = int(np.count_nonzero(buf[:len(contents)] == 10)) + 1
     for _ in range(2):
         ln = np.zeros(max(cap, 1), np.uint64)
         st = np.zeros(max(cap, 1), np.uint64)

@@ -25,12 +25,14 @@ def _build():
     assert os.access(EXE, os.X_OK)
 
 
-def _run(tmp_path, pattern: bytes, data: bytes):
+def _run(tmp_path, pattern: bytes, data: bytes, env=None):
     (tmp_path / "p").write_bytes(pattern)
     (tmp_path / "d").write_bytes(data)
     out = tmp_path / "o"
+    e = dict(os.environ)
+    e.update(env or {})
     p = subprocess.run([EXE, str(tmp_path / "p"), str(tmp_path / "d"), str(out)], capture_output=True, text=True,
-                       timeout=120)
+                       timeout=120, env=e)
     return p, out
 
 
@@ -53,7 +55,7 @@ def test_c_caller_builds_and_fails_loudly_without_gpu(tmp_path):
         pytest.skip("GPU present: covered by the gpu test")
     p, _ = _run(tmp_path, b"error", b"an error\n")
     assert p.returncode != 0
-    assert "dgrep_open" in p.stderr, p.stderr
+    assert "dgrep_pick_device rc=4" in p.stderr, p.stderr  # DGREP_E_HIP: no device at all
 
 
 @pytest.mark.gpu
@@ -61,13 +63,36 @@ def test_c_caller_builds_and_fails_loudly_without_gpu(tmp_path):
 def test_c_caller_plugin_sequence(tmp_path, pattern):
     _build()
     data = dgrep.synth_corpus_host(3 << 20, 31, 0) + b"\nan error at the end"
-    p, out = _run(tmp_path, pattern, data)
+    p, out = _run(tmp_path, pattern, data, {"DGREP_DEVICE": "0"})
     assert p.returncode == 0, p.stderr
     assert "plugin sequence OK" in p.stdout
     ln, st, le = O.grep_map(pattern, data, threads=16)
     want = list(zip(ln.tolist(), st.tolist(), le.tolist()))
     blocks = _parse(out)
-    assert len(blocks) == 2
-    for count, recs in blocks:  # main thread, then the second pthread
+    assert len(blocks) == 3
+    for count, recs in blocks:  # main thread, the second pthread, a second context
         assert count == len(want)
         assert recs == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env,code", [({"DGREP_DEVICE": "99"}, 4), ({"DGREP_DEVICE": "x"}, 1),
+                                      ({"DGREP_WORKER_ID": "7"}, 0)])
+def test_c_caller_device_selection(tmp_path, env, code):
+    """The worker's device (dgrep_pick_device): DGREP_DEVICE=99 is a device
+    that is not present (DGREP_E_HIP = 4), a non-number is DGREP_E_INVALID; a
+    worker id maps to worker_id % device_count."""
+    _build()
+    env = dict(env)
+    env.setdefault("DGREP_DEVICE", None)
+    e = {k: v for k, v in env.items() if v is not None}
+    base = {k: v for k, v in os.environ.items() if k not in ("DGREP_DEVICE", "DGREP_WORKER_ID")}
+    base.update(e)
+    (tmp_path / "p").write_bytes(b"error")
+    (tmp_path / "d").write_bytes(b"an error\nno\n")
+    p = subprocess.run([EXE, str(tmp_path / "p"), str(tmp_path / "d"), str(tmp_path / "o")], capture_output=True,
+                       text=True, timeout=120, env=base)
+    if code == 0:
+        assert p.returncode == 0, p.stderr
+    else:
+        assert p.returncode != 0 and ("dgrep_pick_device rc=%d" % code) in p.stderr, p.stderr

@@ -4,7 +4,7 @@ order, with uneven counts (one rank 10x the others, one rank empty) and a
 non-zero destination rank. The per-rank records come from the oracle here
 (the GPU scan is exercised in tests/test_gpu_parity.py); what is tested is
 the exchange step of bench.py (dgrep/dist.py: count all-gather, then grouped
-send/recv of packed 20-byte records)."""
+send/recv of packed 28-byte records that carry their split id)."""
 import os
 import socket
 
@@ -55,7 +55,7 @@ def _worker(rank, world, port, dst, q):
         # the scan's output arrays are longer than the count (capacity)
         t = [torch.cat([torch.from_numpy(x.astype(dt)), torch.full((7,), -1, dtype=getattr(torch, dt))])
              for x, dt in ((ln, "int64"), (st, "int64"), (le, "int32"))]
-        out = gather_records(t[0], t[1], t[2], len(ln), dst=dst)
+        out = gather_records(t[0], t[1], t[2], len(ln), dst=dst, split=1000 + rank)
         if rank == dst:
             q.put([[x.tolist() for x in triple] for triple in out])
         else:
@@ -89,7 +89,7 @@ def test_gather_records_gloo(world, dst):
     total = 0
     for r in range(world):
         ln, st, le = _records(r)
-        assert got[r] == [ln.tolist(), st.tolist(), le.tolist()], r
+        assert got[r] == [ln.tolist(), st.tolist(), le.tolist(), [1000 + r] * len(ln)], r
         total += len(ln)
     n0 = len(_records(0)[0])
     if world > 2:
@@ -104,9 +104,10 @@ def test_pack_roundtrip():
 
     ln = torch.tensor([1, 2, (1 << 40) + 3], dtype=torch.int64)
     st = torch.tensor([0, 17, (1 << 35) + 9], dtype=torch.int64)
-    le = torch.tensor([5, 0, 2**31 - 1], dtype=torch.int32)
-    p = pack_records(ln, st, le, 3)
+    le = torch.tensor([5, 0, (1 << 33) + 1], dtype=torch.int64)  # a line over 4 GiB
+    p = pack_records(ln, st, le, 3, split=0xFFFFFFFE)
     assert p.numel() * 4 == 3 * REC_BYTES
-    a, b, c = unpack_records(p, 3)
+    a, b, c, d = unpack_records(p, 3)
     assert a.tolist() == ln.tolist() and b.tolist() == st.tolist() and c.tolist() == le.tolist()
+    assert d.tolist() == [0xFFFFFFFE] * 3
     assert pack_records(ln, st, le, 0).numel() == 0

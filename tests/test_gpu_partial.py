@@ -44,14 +44,13 @@ def test_budget_exceeding_patterns_on_gpu(gpu_ctx, pattern):
 
 
 @pytest.mark.parametrize("pattern", PATTERNS)
-def test_forced_partial_every_pattern(gpu_ctx, monkeypatch, pattern):
-    """DGREP_DFA_STATE_BUDGET=3: almost every line becomes a candidate and is
+def test_forced_partial_every_pattern(gpu_ctx, pattern):
+    """State budget 3 (dgrep_compile_budget): almost every line becomes a candidate and is
     decided by the NFA program on the GPU (edges: empty split, no trailing
     '\\n', invalid UTF-8, lines across chunk and tile edges)."""
     import dgrep
 
-    monkeypatch.setenv("DGREP_DFA_STATE_BUDGET", "3")
-    cp = gpu_ctx.load(pattern)
+    cp = gpu_ctx.load(dgrep.CompiledPattern(pattern, state_budget=3))
     if cp.go_syntax_error:
         return
     assert cp.partial, (pattern, cp.nstates)

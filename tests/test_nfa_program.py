@@ -2,7 +2,7 @@
 include/dgrep_blob.h): the blob keeps the first DFA states as a filter and an
 NFA program decides the lines that leave them. On the CPU, both halves are
 interpreted by tests/nfa_runner.py and must reproduce the oracle's Map output
-(grep.go:17-29) bit-exactly. DGREP_DFA_STATE_BUDGET (a test knob read by the
+(grep.go:17-29) bit-exactly. dgrep_compile_budget (a test entry point of the
 compiler) forces the partial form on small patterns, so the NFA program is
 checked on the same random patterns as the DFA (test_compiler.py)."""
 import ctypes
@@ -23,8 +23,7 @@ def _eq(got, want, what):
 
 
 @pytest.mark.parametrize("budget", ["3", "12"])
-def test_partial_program_vs_oracle_random(monkeypatch, budget):
-    monkeypatch.setenv("DGREP_DFA_STATE_BUDGET", budget)
+def test_partial_program_vs_oracle_random(budget):
     rnd = random.Random(1000 + int(budget))
     checked = 0
     for _ in range(300):
@@ -32,7 +31,7 @@ def test_partial_program_vs_oracle_random(monkeypatch, budget):
         if O.compile_status(pat) != O.ORC_OK:
             continue
         try:
-            cp = dgrep.CompiledPattern(pat)
+            cp = dgrep.CompiledPattern(pat, state_budget=int(budget))
         except dgrep.UnsupportedPattern:
             continue
         if not cp.partial:
@@ -80,3 +79,57 @@ def test_blob_info_checks_the_program():
     noflag = bytearray(cp.blob)
     noflag[8:12] = (0).to_bytes(4, "little")
     assert L.dgrep_blob_info_get(bytes(noflag), len(noflag), ctypes.byref(info)) == dgrep.DGREP_E_INVALID
+
+
+def _bad(blob: bytes) -> bool:
+    info = dgrep._BlobInfo()
+    return dgrep.lib().dgrep_blob_info_get(blob, len(blob), ctypes.byref(info)) == dgrep.DGREP_E_INVALID
+
+
+@pytest.mark.parametrize("pattern", [b"[ab]*a[ab]{21}", b"a.{20}$", b"\\bx[ab]*a[ab]{21}"])
+def test_blob_info_rejects_malformed_programs(pattern):
+    """Every field verify_nfa_kernel indexes with is checked on the host
+    (dgrep_blob_info_get, which dgrep_load_dfa calls first): header sizes,
+    decoder children, leaf classes, U+FFFD's class, depths, word flags and
+    position bits beyond npos. A program that fails any of them never reaches
+    the device."""
+    cp = dgrep.CompiledPattern(pattern)
+    assert cp.partial
+    ne = cp.nstates * cp.nclasses
+    off = 288 + 4 * ne  # the program's first word
+    prog = np.frombuffer(cp.blob[off:], dtype=np.uint32).copy()
+    assert not _bad(cp.blob)
+    npos, nw, nrc, nnodes, nctx = (int(x) for x in prog[1:6])
+
+    def with_word(i, v):
+        p = prog.copy()
+        p[i] = np.uint32(v & 0xffffffff)
+        return cp.blob[:off] + p.tobytes()
+
+    assert _bad(with_word(0, 0x12345678))          # magic
+    assert _bad(with_word(1, 257))                 # npos above the maximum
+    assert _bad(with_word(2, nw + 1))              # nw != ceil(npos / 32)
+    assert _bad(with_word(3, nrc + 1))             # size no longer matches the layout
+    assert _bad(with_word(4, nnodes + 1))
+    assert _bad(with_word(5, 2))                   # nctx neither 1 nor 4
+    assert _bad(with_word(6, nrc))                 # U+FFFD's class out of range
+    assert _bad(with_word(7, 2))                   # has_word not a flag
+    child0 = 8
+    assert _bad(with_word(child0 + ord("a"), nnodes))          # interior child beyond the trie
+    assert _bad(with_word(child0 + ord("a"), 0))               # a child back to the root
+    assert _bad(with_word(child0 + ord("a"), (-2 - nrc)))      # leaf class beyond nrc
+    depth0 = child0 + nnodes * 256
+    assert _bad(with_word(depth0, 1))                          # the root holds no pending byte
+    word0 = depth0 + nnodes
+    assert _bad(with_word(word0, 7))
+    has0 = word0 + nrc
+    if npos % 32:
+        assert _bad(with_word(has0 + nw - 1, 1 << 31))         # a position bit beyond npos
+    # truncated, and a DFA byte class / transition out of range
+    assert _bad(cp.blob[:-4])
+    bc = bytearray(cp.blob)
+    bc[32 + ord("a")] = cp.nclasses
+    assert _bad(bytes(bc))
+    tr = bytearray(cp.blob)
+    tr[288:292] = (cp.nstates).to_bytes(4, "little")
+    assert _bad(bytes(tr))

@@ -115,3 +115,41 @@ def test_key_and_json_format():
     # HTML escaping, control characters, invalid UTF-8 and U+2028 as encoding/json does
     assert O.json_kv(b"<&>", b"\t\"\\\x01\xff\xe2\x80\xa8") == \
         b'{"Key":"\\u003c\\u0026\\u003e","Value":"\\t\\"\\\\\\u0001\\ufffd\\u2028"}\n'
+
+
+def test_memoized_matcher_equals_pike_vm_random():
+    """orc_map_mt decides lines with the memoized Pike VM (a lazy DFA over the
+    same program, oracle/goregexp.c orc_matcher_*); it must give exactly the
+    plain Pike VM's verdicts (orc_map): random patterns from the compiler
+    tests (Unicode classes, (?i), \\b, anchors, repeats) over random lines with
+    invalid UTF-8, many lines per split so the cached transitions are reused."""
+    from test_compiler import ALPHA, _rand_pattern
+
+    rnd = random.Random(4242)
+    checked = 0
+    for _ in range(400):
+        pat = _rand_pattern(rnd).encode()
+        if O.compile_status(pat) == O.ORC_EUNSUPPORTED:
+            continue
+        data = b"".join(rnd.choice(ALPHA) for _ in range(rnd.randint(0, 600)))
+        a = O.grep_map(pat, data)
+        b = O.grep_map(pat, data, threads=2)
+        for x, y in zip(a, b):
+            assert list(x) == list(y), pat
+        checked += 1
+    assert checked > 300
+
+
+def test_memoized_matcher_cache_flush():
+    """A pattern whose lazy DFA outgrows the matcher's cache (2^15 states for
+    [ab]*a[ab]{14}): the cache is flushed mid-line and rebuilt, verdicts equal
+    the plain Pike VM's."""
+    rnd = random.Random(7)
+    lines = [bytes(rnd.choice(b"ab") for _ in range(rnd.randint(0, 300))) for _ in range(300)]
+    data = b"\n".join(lines)
+    for pat in (b"[ab]*a[ab]{14}", b"a[ab]{12}b$"):
+        a = O.grep_map(pat, data)
+        b = O.grep_map(pat, data, threads=2)
+        assert len(a[0]) > 10
+        for x, y in zip(a, b):
+            assert list(x) == list(y), pat
