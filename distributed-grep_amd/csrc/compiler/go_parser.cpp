@@ -283,19 +283,22 @@ class GoParser {
       }
     }
     if (!found) {
-      // Go also accepts unicode.Scripts names (\p{Greek}); the script tables
-      // are not available offline, so a plausible script name is refused as
-      // unsupported rather than treated as the syntax error it may not be.
-      bool plausible = name.size() > 1;
-      for (char ch : name)
-        if (!((ch >= 'a' && ch <= 'z') || (ch >= 'A' && ch <= 'Z') || ch == '_')) plausible = false;
-      if (!plausible) { syntax("invalid character class range"); return -1; }
-      unsupported("unicode script classes");
-      tab.add(0, kMaxRune);
+      // [Go stdlib] regexp/syntax unicodeTable: unicode.Categories first, then
+      // unicode.Scripts (with unicode.FoldScript as the fold table)
+      for (int i = 0; i < dg_nscripts; ++i) {
+        if (name == dg_scripts[i].name) {
+          for (int j = 0; j < dg_scripts[i].n; ++j)
+            tab.add(int32_t(dg_scripts[i].r[2 * j]), int32_t(dg_scripts[i].r[2 * j + 1]));
+          folds = dg_scripts[i].fold != 0;
+          found = true;
+          break;
+        }
+      }
     }
+    if (!found) { syntax("invalid character class range"); return -1; }
     if ((flags_ & kFoldCase) && folds) {
-      // [Go stdlib] unicode.FoldCategory: the runes outside the category that
-      // simple-fold to runes inside it -- the category's orbit closure
+      // [Go stdlib] unicode.FoldCategory / FoldScript: the runes outside the
+      // table that simple-fold to runes inside it -- the table's orbit closure
       RuneSet closed;
       tab.normalize();
       for (const auto& rg : tab.ranges())

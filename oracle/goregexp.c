@@ -184,7 +184,6 @@ static Node* p_op(Parser* p, int op) {
   return n;
 }
 static void fail(Parser* p, const char* m) { if (!p->err) { p->err = 1; p->msg = m; } }
-static void unsup(Parser* p, const char* m) { if (!p->unsupported) { p->unsupported = 1; if (!p->err) p->msg = m; } }
 
 /* nextRune (parse.go): invalid UTF-8 is an error; empty input gives RuneError */
 static int next_rune(Parser* p, const unsigned char** t, const unsigned char* end) {
@@ -333,21 +332,19 @@ static int parse_unicode_class(Parser* p, const unsigned char** t, const unsigne
         break;
       }
     }
-    if (!found && nl > 1) {
-      /* Go accepts script names (unicode.Scripts); we cannot tell a real
-       * script from a typo without the table: valid-looking names are
-       * "unsupported", never silently "no match". */
-      int ok = 1;
-      for (size_t i = 0; i < nl; i++) {
-        unsigned char ch2 = name[i];
-        if (!((ch2 >= 'a' && ch2 <= 'z') || (ch2 >= 'A' && ch2 <= 'Z') || ch2 == '_')) ok = 0;
+    /* unicodeTable (parse.go): unicode.Categories, then unicode.Scripts */
+    for (int i = 0; !found && i < orc_nscripts; i++) {
+      if (strlen(orc_scripts[i].name) == nl && memcmp(orc_scripts[i].name, name, nl) == 0) {
+        for (int j = 0; j < orc_scripts[i].n; j++)
+          cls_push(&tmp, (int)orc_scripts[i].r[2 * j], (int)orc_scripts[i].r[2 * j + 1]);
+        fold_tab = orc_scripts[i].fold;
+        found = 1;
       }
-      if (ok) { unsup(p, "unicode script class"); cls_push(&tmp, 0, MAXRUNE); found = 1; }
     }
   }
   if (!found) { free(tmp.r); fail(p, "invalid character class range (unicode name)"); return -1; }
   if ((p->flags & F_FOLD) && fold_tab) {
-    /* FoldCategory (parseUnicodeClass): add the runes that simple-fold into the table */
+    /* FoldCategory / FoldScript (parseUnicodeClass): add the runes that simple-fold into the table */
     Class closed = {0};
     cls_clean(&tmp);
     for (int i = 0; i < tmp.n; i += 2) {

@@ -15,7 +15,13 @@ present here and agrees with Go on that case:
   ``\\v``), no ``{,n}``, no Unicode classes);
 * ``gnu-grep``: ``LC_ALL=C grep -a -n -E`` for ERE-compatible patterns (grep
   never reports the empty piece after a trailing '\\n'; that piece is checked
-  against the oracle alone).
+  against the oracle alone);
+* ``perl-re``: perl 5.34's regex engine (Unicode 13.0, like Go 1.18) for
+  patterns built only from Unicode script / category classes, literals and
+  ``+ * ?``, without (?i) (perl folds fully, Go simply): each piece decoded as
+  Go decodes it (an invalid byte is U+FFFD), ``\\p{Name}`` of a script given to
+  perl as ``\\p{Script=Name}`` (perl's bare ``\\p{Greek}`` means
+  Script_Extensions).
 
 A vector with no applicable witness (Unicode case folding, invalid UTF-8,
 Go syntax errors, ...) is still written, marked ``"witnesses": []`` — parity
@@ -82,6 +88,59 @@ def _grep_lines(pattern: bytes, data: bytes):
     return [int(ln.split(b":", 1)[0]) for ln in p.stdout.split(b"\n") if ln]
 
 
+_SCRIPT_CLASS = re.compile(rb"\\[pP]\{(\^?)([A-Za-z_]+)\}")
+
+
+def _perl_ok(pattern: bytes, data: bytes) -> bool:
+    if shutil.which("perl") is None or O.compile_status(pattern) != O.ORC_OK:
+        return False
+    if not _SCRIPT_CLASS.search(pattern):
+        return False
+    rest = _SCRIPT_CLASS.sub(b"", pattern)
+    return re.fullmatch(rb"[A-Za-z0-9 +*?^$]*", rest) is not None
+
+
+def _go_decode(line: bytes) -> str:
+    """Go's utf8.DecodeRune walk: a byte that does not start a valid sequence is U+FFFD, width 1."""
+    out, i = [], 0
+    while i < len(line):
+        for w in (1, 2, 3, 4):
+            try:
+                ch = line[i:i + w].decode("utf-8")
+            except UnicodeDecodeError:
+                continue
+            if len(ch) == 1:
+                out.append(ch)
+                i += w
+                break
+        else:
+            out.append("\ufffd")
+            i += 1
+    return "".join(out)
+
+
+def _perl_lines(pattern: bytes, data: bytes):
+    categories = {"L", "Lu", "Ll", "Lt", "Lm", "Lo", "M", "Mn", "Mc", "Me", "N", "Nd", "Nl", "No", "P", "S", "Z",
+                  "C", "Cc", "Cf", "Co", "Cs", "Any"}
+
+    def conv(m):
+        neg, name = m.group(1), m.group(2)
+        if name.decode() in categories:
+            return m.group(0)
+        return b"\\" + m.group(0)[1:2] + b"{" + neg + b"Script=" + name + b"}"
+
+    pp = _SCRIPT_CLASS.sub(conv, pattern).decode()
+    lines = [_go_decode(x) for x in data.split(b"\n")]
+    prog = 'binmode STDIN, ":encoding(UTF-8)"; my $re = qr/$ARGV[0]/; my $n = 0; ' \
+           'while (my $l = <STDIN>) { chomp $l; $n++; print "$n\\n" if $l =~ $re; }'
+    inp = "\n".join(lines) + "\n"
+    p = subprocess.run(["perl", "-e", prog, pp], input=inp.encode("utf-8", "surrogatepass"), stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE)
+    if p.returncode != 0:
+        return None
+    return [int(x) for x in p.stdout.split()]
+
+
 _INPUTS = []
 
 
@@ -108,6 +167,11 @@ def vector(name: str, filename: str, pattern: bytes, data: bytes):
             want = [x for x in ln if not (x == last and (data.endswith(b"\n") or not data))]
             assert g == want, (name, "gnu-grep disagrees with the oracle", g[:10], want[:10])
             witnesses.append("gnu-grep")
+    if _perl_ok(pattern, data):
+        g = _perl_lines(pattern, data)
+        if g is not None:
+            assert g == ln, (name, "perl-re disagrees with the oracle", g[:10], ln[:10])
+            witnesses.append("perl-re")
     fn = filename.encode()
     keys = [O.format_key(fn, x) for x in ln]
     values = [data[s:s + n] for s, n in zip(st, le)]
@@ -139,6 +203,7 @@ EDGE_DATA = [
     b"a\r\nerror\r\n", b"key\nk\n", b"an error\n" * 3 + b"no", b"2024-01-02T03:04:05.678 WARN auth_svc: x\n",
     b"\xff\xfe\n\xe2\x82\xac\n\xe2\x82\n\xef\xbf\xbd\n", b"\xe2\x84\xaaey\n\xc5\xbftop\nKEY\nstop\n",
     b"a" * 3000 + b"error" + b"b" * 3000 + b"\nerror", b"tab\there\nvt\x0bhere\n", b"\x00error\x00\n",
+    "Αθήνα error\nµ micro\nͅ ypogegrammeni\nι iota\n中文 log\nМосква\nK kelvin\n123\n\n".encode() + b"\xce\xff\n",
 ]
 
 EDGE_PATTERNS = [
@@ -146,6 +211,8 @@ EDGE_PATTERNS = [
     b"\\berror\\b", b"\\Berr", b"e(r|x)+o", b"[^a-z ]{3}", b"\\x{FFFD}", b"\\x{20AC}", b"\\s", b"\\d+",
     b"\\w{4}", b"(WARN|ERROR) [a-z_]+", b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"a**", b"(", b"x{1001}",
     b"\\r$", b"(?s).", b"[[:upper:]]", b"\\pL", b"[a-c]+r",
+    b"\\p{Greek}", b"(?i)\\p{Greek}", b"\\P{Latin}", b"^\\p{Han}+", b"\\p{Cyrillic}+$", b"(?i)\\p{Common}",
+    b"\\p{Greek} \\p{Latin}+", b"\\p{Bogus}",
 ]
 
 

@@ -33,7 +33,8 @@ def test_exports_every_declared_symbol():
 
 def test_compile_errors_and_unsupported():
     with pytest.raises(dgrep.UnsupportedPattern):
-        dgrep.CompiledPattern("\\p{Greek}")
+        dgrep.CompiledPattern("(" * 1001 + "a" + ")" * 1001)  # nesting beyond 1000: refused, never guessed
+    assert dgrep.CompiledPattern("\\p{Greek}").nstates > 1
     cp = dgrep.CompiledPattern("(")
     assert cp.go_syntax_error
     assert "syntax" in cp.message

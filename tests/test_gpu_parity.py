@@ -598,3 +598,32 @@ def test_unicode_case_folding(gpu_ctx, pattern):
     pattern = pattern.encode()
     n = _check(gpu_ctx, pattern, data, threads=16)
     assert n > 0
+
+
+SCRIPT_PATTERNS = [b"(?i)\\p{Greek}+", b"\\P{Latin}", b"\\p{Han}", b"\\p{Cyrillic}[a-z]", b"(?i)\\p{Common}{3}$",
+                   b"\\p{Greek}\\P{Greek}", b"(?i)\\P{Inherited}\\p{Inherited}"]
+
+
+def _multiscript_split(seed, n_lines):
+    rnd = random.Random(seed)
+    words = ["error", "Αθήνα", "αβγ", "ΣΟΦΙΑ", "µ", "ͅ", "ι", "ι", "中文", "日本語", "Москва", "дом",
+             "K", "K", "ß", "ẞ", "123", "é", "́", "၀0", "\U00010300", " ", "-", ":"]
+    lines = []
+    for _ in range(n_lines):
+        lines.append("".join(rnd.choice(words) for _ in range(rnd.randint(0, 12))).encode() +
+                     (b"\xff" if rnd.random() < 0.05 else b""))
+    return b"\n".join(lines)
+
+
+@pytest.mark.parametrize("pattern", SCRIPT_PATTERNS)
+def test_unicode_script_classes(gpu_ctx, pattern):
+    """\\p{Script} / \\P{Script} (unicode.Scripts, Unicode 13.0) and (?i) with
+    unicode.FoldScript, over lines mixing Greek, Latin, Cyrillic, Han, combining
+    marks and invalid UTF-8, at small size and across chunk/tile edges."""
+    import dgrep
+
+    for size in (0, 2000, 40000):
+        _check(gpu_ctx, pattern, _multiscript_split(size, size // 10 + 1), threads=8)
+    data = bytearray(dgrep.synth_corpus_host(2 << 20, 13, 0))
+    data += _multiscript_split(1, 5000)
+    _check(gpu_ctx, pattern, bytes(data), threads=16)
