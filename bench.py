@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 STAGED_LINE_BYTES = 16  # StagedLine written by the scan kernel per match
-LEN_DTYPE = "int32"  # torch dtype of the length array dgrep_scan_device writes (uint32 in dgrep.h)
+LEN_DTYPE = "int64"  # torch dtype of the length array dgrep_scan_device writes (uint64 in dgrep.h)
 
 WORKLOADS = {
     # BASELINE.json configs[0] / SURVEY §8d C1: the reference's CPU-runnable case
@@ -50,6 +50,14 @@ WORKLOADS = {
     # SURVEY §8d C5 / BASELINE.json configs[4]: 8 splits x 32 GiB, seeds 100-107
     "c5": dict(pattern="error", seed=100, rank_seed_step=1, kind=0, gib=32.0,
                desc="C5: one 32 GiB synthetic log split per GPU (seed 100 + rank), literal 'error'"),
+    # long lines (kind 2: geometric, 4 MiB mean, each followed by a page of log
+    # lines; kind 3: the same after one newline-free 1 GiB line): lanes park a
+    # line that runs past the next chunk, the long-line kernels finish it
+    "long": dict(pattern="error", seed=7, kind=2, gib=16.0,
+                 desc="long lines: 16 GiB split (seed 7) of 4 MiB-mean lines (no line limit) between pages of log "
+                      "lines, literal 'error'"),
+    "long1g": dict(pattern="error", seed=8, kind=3, gib=16.0,
+                   desc="long lines + one newline-free 1 GiB line: 16 GiB split (seed 8), literal 'error'"),
     # a dense Sheng line (~60 % of lines match): the lane chunk adapts to the match density
     "dense": dict(pattern="e", seed=2, kind=0, gib=16.0,
                   desc="dense: 16 GiB split (seed 2), literal 'e' (most lines match)"),
@@ -305,6 +313,7 @@ def main():
                 "scan_ms_avg": round(float(np.mean([x["scan_ms"] for x in stats])), 4),
                 "candidates_dropped": int(st["candidates"]),
                 "overflow_lanes": int(st["overflow_lanes"]),
+                "pending_lines": int(st["pending"]),
                 "timing": "HIP events on the launch stream around the scan kernel, the overflow pass and (filter "
                           "stepper) the candidate verification (dgrep_last_kernel_ms), averaged over the timed steps",
                 "algorithmic_bytes_per_launch": int(n + STAGED_LINE_BYTES * count),
@@ -446,7 +455,7 @@ def check_records(buf, n, line_t, start_t, len_t):
     if line_t.numel() == 0:
         return
     st = start_t.to(torch.int64)
-    en = st + len_t.to(torch.int64) % (1 << 32)
+    en = st + len_t.to(torch.int64)
     assert bool((st >= 0).all()) and bool((en <= n).all()), "record outside the split"
     step = 1 << 30  # torch.nonzero mis-sizes its output past 2**31 elements: 1 GiB pieces
     nlpos = torch.cat([torch.nonzero(buf[o:min(n, o + step)] == 10).flatten() + o for o in range(0, n, step)])

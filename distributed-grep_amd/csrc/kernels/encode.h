@@ -10,7 +10,7 @@ struct EncodeArgs {
   uint64_t n;                 // its bytes (aligned 16-B reads never pass them)
   const uint64_t* line_no;    // scan records, ascending line order
   const uint64_t* start;
-  const uint32_t* len;
+  const uint64_t* len;
   uint64_t count;
   const uint8_t* fname_json;  // the filename, JSON-escaped, without quotes (device)
   uint32_t fname_json_len;

@@ -5,14 +5,28 @@
 namespace dgrep {
 
 // One matching line as produced by a tile, before global ordering.
-// `rel` = number of '\n' between the tile start and the line start, so the
-// 1-based line number (application/grep.go:25 `line_number+1`) is
-// newlines_before_tile + rel + 1.
+// meta = rel | flags | len_hi: `rel` (bits 0-21) = number of '\n' between the
+// tile start and the line start, so the 1-based line number
+// (application/grep.go:25 `line_number+1`) is newlines_before_tile + rel + 1
+// (a tile is at most 64 x 32 KiB, so rel < 2^21); bit 22 = filter CANDIDATE
+// (verified afterwards); bit 23 = PENDING long line (len_lo = its index in the
+// pending list, resolved afterwards); bits 24-31 = bits 32-39 of the length
+// (lines up to 1 TiB: more than HBM holds).
 struct StagedLine {
   uint64_t start;  // absolute byte offset of the line in the split
-  uint32_t len;    // bytes, '\n' excluded
-  uint32_t rel;
+  uint32_t len_lo; // bytes, '\n' excluded (low 32 bits)
+  uint32_t meta;
 };
+constexpr uint32_t kRelBits = 22;
+constexpr uint32_t kMetaCand = 1u << 22;
+constexpr uint32_t kMetaPend = 1u << 23;
+__host__ __device__ inline uint32_t meta_of(uint32_t rel, uint64_t len, bool cand) {
+  return rel | (cand ? kMetaCand : 0u) | (uint32_t(len >> 32) << 24);
+}
+__host__ __device__ inline uint64_t staged_len(const StagedLine& L) {
+  return uint64_t(L.len_lo) | (uint64_t(L.meta >> 24) << 32);
+}
+__host__ __device__ inline uint32_t staged_rel(const StagedLine& L) { return L.meta & ((1u << kRelBits) - 1u); }
 
 // Per-tile bookkeeping written by the scan kernel.
 struct TileInfo {
@@ -30,6 +44,22 @@ struct OverflowLane {
   uint32_t pad;
 };
 
+// A long line the scan parked (see park_pending): its start, the chunk boundary
+// where the lane stopped and its state there (as an index of the stepper's
+// state -> blob state table); the long-line kernels fill end, len, matched.
+struct PendingLine {
+  uint64_t line_start;
+  uint64_t resume;
+  uint32_t state;
+  uint32_t matched;
+  uint64_t end;
+  uint64_t len;
+};
+// a segment of a parked line's remaining bytes (long_map_kernel)
+struct LongSeg {
+  uint64_t begin, end;
+};
+
 struct ScanArgs {
   const uint8_t* data;
   uint64_t n;
@@ -42,7 +72,6 @@ struct ScanArgs {
   uint64_t capacity;      // staging/output capacity in lines
   unsigned long long* counter;  // staging append counter
   TileInfo* tiles;
-  uint32_t* status;       // error bits (kStatus*)
   OverflowLane* overflow;
   uint64_t overflow_cap;
   unsigned long long* overflow_count;
@@ -62,6 +91,34 @@ struct ScanArgs {
   // HBM the lane moves its full LDS slots to (nullptr: no spilling)
   uint2* spill;
   uint32_t spill_per_lane;
+  // slot mode: per resident thread and stream, the real length of the lane's
+  // last record when its LDS slot holds kSlotLong (or its pending index)
+  uint64_t* tails;
+  // <= 256-state steppers: '\n' count per chunk, and the pending list of parked
+  // long lines (pend nullptr: a long line is read to its end by its lane)
+  uint32_t* chunk_nl;
+  PendingLine* pend;
+  uint64_t pend_cap;
+  unsigned long long* pend_count;
+};
+
+// the long-line kernels' arguments (long_end / long_map / long_fin)
+struct LongArgs {
+  const uint8_t* data;
+  uint64_t n;
+  uint64_t chunk;    // lane chunk bytes of the scan
+  uint64_t nchunks;
+  const uint32_t* chunk_nl;
+  PendingLine* pend;
+  uint64_t npend;
+  const uint32_t* st2id;  // PendingLine::state -> blob state
+  const uint8_t* tbl;     // u8 [S][256]: blob state x byte -> blob state
+  uint32_t nstates;       // S <= 256
+  uint32_t start_m;       // blob id
+  const LongSeg* seg;
+  uint64_t nseg;
+  const uint64_t* seg_off;  // [npend + 1]: line i's segments
+  uint8_t* segmap;          // [nseg][256]
 };
 
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids
@@ -84,13 +141,17 @@ struct VerifyArgs {
   // '\n' -> start_m; UINT32_MAX: none): a candidate that reaches it matches,
   // so verify_kernel stops reading the line there
   uint32_t matched;
+  // resolved pending long lines (StagedLine kMetaPend: len_lo = index)
+  const PendingLine* pend;
 };
 
-// A staged line whose len has this bit set is a filter CANDIDATE (kStepFilter):
-// verify_kernel re-runs it on the whole DFA and keeps it only if it matches.
+// LDS slot records (8 B: start16 | rel16, then w1): w1 = the line's length with
+// bit 31 the filter CANDIDATE flag; a length of kSlotLong or more (only a
+// lane's LAST owned line can reach past its <= 32 KiB chunk) is stored as
+// kSlotLong and the lane keeps the real length (or its pending index) in
+// LaneRun::tail.
 constexpr uint32_t kCandidateBit = 0x80000000u;
-
-enum : uint32_t { kStatusLineTooLong = 1u, kStatusCandidateTooLong = 2u };
+constexpr uint32_t kSlotLong = 0x7fffffffu;
 
 constexpr int kScanThreads = 256;  // 4 waves per workgroup
 constexpr int kTileLanes = 64;     // a tile is one wave's 64 chunks

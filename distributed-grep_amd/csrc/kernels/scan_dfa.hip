@@ -17,8 +17,13 @@
 //     don't-care state, which the first '\n' resets -- through its chunk and on
 //     past the chunk end until the first '\n' at or after the end (the last
 //     owned line's terminator) or the end of the split. No lane ever waits for
-//     another lane's state; a line longer than a chunk is simply run to its end
-//     by the lane that owns it.
+//     another lane's state. A lane whose chunk holds no '\n' owns no line and
+//     stops at its chunk end. Long lines: on the <= 256-state steppers a lane
+//     whose last line is still open two chunks past its chunk start parks it
+//     as PENDING (state + position); the long-line kernels (long_end_kernel,
+//     long_map_kernel, long_fin_kernel) then find its end from the per-chunk
+//     '\n' counts and run the DFA over it in parallel -- per-piece transition
+//     maps, composed in order -- instead of one lane reading on alone.
 //   * Per 4-byte word: 4 DFA steps by one of two steppers (below), newline
 //     bookkeeping by SWAR on the word, and a matching line is detected by
 //     "state == START_M" (rare path).
@@ -198,6 +203,26 @@ struct StepSheng8 {
   // renumbering): one max over the word's four states replaces four compares
   __device__ __forceinline__ static bool any4(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t M) {
     return max(max(s0, s1), max(s2, s3)) >= M * 0x01010101u;
+  }
+  // map <- bytes 0..lim of the word applied to the 8-state map (lo: states 0-3,
+  // hi: states 4-7; byte s = the state reached from state s); one v_perm per
+  // byte and half
+  __device__ __forceinline__ void compose(const Pre& p, uint32_t lim, uint32_t& lo, uint32_t& hi) const {
+    lo = sel(p.m0, lo);
+    hi = sel(p.m0, hi);
+    const uint32_t l1 = sel(p.m1, lo), h1 = sel(p.m1, hi);
+    lo = lim >= 1 ? l1 : lo;
+    hi = lim >= 1 ? h1 : hi;
+    const uint32_t l2 = sel(p.m2, lo), h2 = sel(p.m2, hi);
+    lo = lim >= 2 ? l2 : lo;
+    hi = lim >= 2 ? h2 : hi;
+    const uint32_t l3 = sel(p.m3, lo), h3 = sel(p.m3, hi);
+    lo = lim >= 3 ? l3 : lo;
+    hi = lim >= 3 ? h3 : hi;
+  }
+  __device__ __forceinline__ void compose_byte(uint32_t b, uint32_t& lo, uint32_t& hi) const {
+    lo = sel(V[b], lo);
+    hi = sel(V[b], hi);
   }
 };
 
@@ -427,6 +452,9 @@ struct LaneRun {
   bool term;         // the terminating '\n' at or after the chunk end was consumed
   uint32_t nev;      // matching lines emitted
 };
+// ScanArgs::tails entry of a lane whose last record's slot holds kSlotLong: the
+// real length, or (bit 63) a PENDING line's index in the pending list
+constexpr uint64_t kTailPending = 1ull << 63;
 
 template <int E, bool DIRECT>
 struct Emitter {
@@ -437,22 +465,28 @@ struct Emitter {
   uint32_t nl_prefix;    // '\n' between tile start and chunk start (direct mode)
   uint2* spill = nullptr;    // slot mode: this lane's HBM spill area (nullptr: none)
   uint32_t spill_cap = 0;    // its records
+  uint64_t* tail = nullptr;  // slot mode: this lane's ScanArgs::tails entry
 
-  // cand: a filter candidate (kCandidateBit in len, verified afterwards)
+  // cand: a filter candidate (verified afterwards)
   __device__ __forceinline__ void operator()(LaneRun& r, uint64_t q, int64_t start, uint32_t rel,
                                              bool cand = false) const {
     const uint64_t len = q - uint64_t(start);
-    const uint32_t lw = uint32_t(len) | (cand ? kCandidateBit : 0u);
     if (DIRECT) {
       const uint64_t o = out_base + r.nev;
       if (o < a->capacity) {
         StagedLine L;
         L.start = cs + uint64_t(start);
-        L.len = lw;
-        L.rel = nl_prefix + rel;
+        L.len_lo = uint32_t(len);
+        L.meta = meta_of(nl_prefix + rel, len, cand);
         a->staging[o] = L;
       }
     } else {
+      // only the lane's last owned line can reach past its <= 32 KiB chunk
+      uint32_t lw = uint32_t(len) | (cand ? kCandidateBit : 0u);
+      if (len >= kSlotLong) {
+        lw = kSlotLong | (cand ? kCandidateBit : 0u);
+        *tail = len;
+      }
       // start < C and rel < C fit 16 bits each
       const uint32_t w0 = uint32_t(start) | (rel << 16);
       if (r.nev < uint32_t(E)) {
@@ -465,8 +499,19 @@ struct Emitter {
         spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
       }
     }
-    if (len > 0xffffffffull) atomicOr(a->status, kStatusLineTooLong);
-    if (cand && len >= uint64_t(kCandidateBit)) atomicOr(a->status, kStatusCandidateTooLong);
+    ++r.nev;
+  }
+  // slot mode: the lane's last owned line is left PENDING (pending-list index
+  // idx), resolved after the scan (long_end / long_map / long_fin kernels)
+  __device__ __forceinline__ void pending(LaneRun& r, int64_t start, uint32_t rel, uint64_t idx) const {
+    const uint32_t w0 = uint32_t(start) | (rel << 16);
+    *tail = kTailPending | idx;
+    if (r.nev < uint32_t(E)) {
+      slots[r.nev * 2 + 0] = w0;
+      slots[r.nev * 2 + 1] = kSlotLong;
+    } else if (r.nev - uint32_t(E) < spill_cap) {
+      spill[r.nev - uint32_t(E)] = make_uint2(w0, kSlotLong);
+    }
     ++r.nev;
   }
   // The same for a line wholly inside the lane's chunk (start < q < C <= 32 KiB):
@@ -490,8 +535,8 @@ struct Emitter {
       if (o < a->capacity) {
         StagedLine L;
         L.start = cs + uint64_t(start);
-        L.len = lw;
-        L.rel = nl_prefix + rel;
+        L.len_lo = q - start;
+        L.meta = meta_of(nl_prefix + rel, 0, cand);
         a->staging[o] = L;
       }
     } else {
@@ -746,9 +791,10 @@ __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8
                          LaneRun& r, uint32_t& nl_chunk, bool& snap, const Emitter<E, DIRECT>& emit) {
   for (; pos < avail; ++pos) {
     if (pos == C) { nl_chunk = r.nl; snap = true; }
-    if (pos >= C && r.term) return;
+    if (pos >= C && (r.term || !r.seen)) return;
     const uint32_t b = p[pos];
     const uint32_t s1 = st.byte(r.s, b);
+
     if (b == '\n') {
       if (Step::is(s1, M) && r.seen && !(pos >= C && r.term)) emit(r, pos, r.prev_nl + 1, r.nl, cand_of(st, s1));
       r.seen = true;
@@ -771,6 +817,51 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
   r.nev = 0;
 }
 
+// The <= 256-state steppers park long lines in the main scan (slot mode; the
+// overflow pass re-runs chunks in direct mode and reads such a line on). The
+// filter's CAND state has no exact DFA state to resume from, and the wide
+// stepper is a forced test path: their lanes read a long line to its end.
+template <class Step, bool DIRECT>
+constexpr bool track_long() {
+  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepTable) && !DIRECT;
+}
+// the parked state as an index of ScanArgs::pend_states (stepper encoding ->
+// DFA state of the blob)
+template <class Step>
+__device__ __forceinline__ uint32_t park_index(const ScanArgs& a, uint32_t s) {
+  if constexpr (Step::kKind == kStepSheng8) return s & 0xffu;
+  else if constexpr (Step::kKind == kStepPair) return (s - kPairT2) / a.pair_div;
+  else return s;
+}
+
+// Past the chunk end the lane stops once its last owned line is finished
+// (term) -- or at once if it owns no line at all (no '\n' in its chunk: the
+// chunk lies inside a line an earlier lane owns).
+__device__ __forceinline__ bool lane_done(uint64_t pos, uint64_t C, const LaneRun& r) {
+  return pos >= C && (r.term || !r.seen);
+}
+
+// The lane's last line is still open at 2 C (it started in the lane's chunk and
+// crossed the whole next one): park it as PENDING -- state and position go to
+// the pending list, the lane's record for it is resolved by the long-line
+// kernels -- instead of reading on alone.
+template <class Step, int E>
+__device__ __forceinline__ void park_pending(const ScanArgs& a, uint64_t cs, uint64_t pos, LaneRun& r,
+                                             const Emitter<E, false>& emit) {
+  const unsigned long long idx = atomicAdd(a.pend_count, 1ull);
+  if (idx < a.pend_cap) {
+    PendingLine P;
+    P.line_start = cs + uint64_t(r.prev_nl + 1);
+    P.resume = cs + pos;
+    P.state = park_index<Step>(a, r.s);
+    P.matched = 0;
+    P.len = 0;
+    a.pend[idx] = P;
+  }
+  emit.pending(r, r.prev_nl + 1, r.nl, idx);
+  r.term = true;
+}
+
 // Runs a lane (see file comment) from chunk-relative position pos0 over
 // BK-byte blocks with direct per-lane loads, prefetching the next block while
 // the current one is stepped (two register buffers, ping-pong). Returns the
@@ -786,33 +877,43 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
     if (!r.term && r.seen && Step::is(se, M)) emit(r, avail, r.prev_nl + 1, r.nl, cand_of(st, se));
     return r.nl;
   }
+
   const uint8_t* __restrict__ p = a.data + cs;
   uint32_t nl_chunk = 0;
   bool snap = false;
   uint64_t pos = pos0;
   uint4 A[BK / 16], B[BK / 16];
+  constexpr bool kTrack = track_long<Step, DIRECT>();
+  const bool park = kTrack && a.pend != nullptr;
   if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
+  // a block inside the chunk goes through the map-tracking copy while any lane
+  // of the wave still looks for its chunk's first '\n' (wave-uniform branch)
+#define DG_STEP(V) run_block<BK>(st, M, V, pos, uint64_t(C), r, emit);
+#define DG_CHECK                                                                           \
+  if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }                                \
+  if (lane_done(pos, uint64_t(C), r)) break;                                               \
+  if constexpr (kTrack) {                                                                  \
+    if (park && pos == 2 * uint64_t(C)) {                                                  \
+      park_pending<Step, E>(a, cs, pos, r, emit);                                          \
+      break;                                                                               \
+    }                                                                                      \
+  }                                                                                        \
+  if (pos + BK > avail) {                                                                  \
+    run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);                  \
+    break;                                                                                 \
+  }
   for (;;) {
-    if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
-    if (pos >= uint64_t(C) && r.term) break;
-    if (pos + BK > avail) {
-      run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);
-      break;
-    }
+    DG_CHECK
     load_block<BK>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
-    run_block<BK>(st, M, A, pos, uint64_t(C), r, emit);
+    DG_STEP(A)
     pos += BK;
-
-    if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }
-    if (pos >= uint64_t(C) && r.term) break;
-    if (pos + BK > avail) {
-      run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);
-      break;
-    }
+    DG_CHECK
     load_block<BK>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
-    run_block<BK>(st, M, B, pos, uint64_t(C), r, emit);
+    DG_STEP(B)
     pos += BK;
   }
+#undef DG_STEP
+#undef DG_CHECK
   if (!snap) nl_chunk = r.nl;
   return nl_chunk;
 }
@@ -924,8 +1025,11 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
 #pragma unroll
     for (int k = 0; k < S; ++k) cs[k] = t * kTile + (uint64_t(k) * kTileLanes + uint64_t(lane)) * uint64_t(C);
     const bool full = (t + 1) * kTile <= a.n;  // wave-uniform: the whole tile lies inside the split
+    uint64_t* const tails = a.tails + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * S;
     if constexpr (S == 2) {
-      const Emitter<E, false> e0{&a, slots, cs[0], 0, 0}, e1{&a, slots + E * 2, cs[1], 0, 0};
+      Emitter<E, false> e0{&a, slots, cs[0], 0, 0}, e1{&a, slots + E * 2, cs[1], 0, 0};
+      e0.tail = tails;
+      e1.tail = tails + 1;
       if (full) {
         run_lane2<Tune<Step>::C, BK>(a, st, cs[0], cs[1], r[0], r[1], e0, e1, nlc[0], nlc[1]);
       } else {
@@ -934,11 +1038,21 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
       }
     } else {
       Emitter<E, false> em{&a, slots, cs[0], 0, 0};
+      em.tail = tails;
       if (a.spill) {
         em.spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane;
         em.spill_cap = a.spill_per_lane;
       }
       nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
+    }
+    if constexpr (track_long<Step, false>()) {
+      // '\n' per chunk (chunk index = t * 64 S + 64 k + lane): where the long-line
+      // kernels look for a parked line's end
+      if (a.chunk_nl) {
+#pragma unroll
+        for (int k = 0; k < S; ++k)
+          if (cs[k] < a.n) a.chunk_nl[t * kTileLanes * S + uint64_t(k) * kTileLanes + uint64_t(lane)] = nlc[k];
+      }
     }
 
     // tile-wide exclusive scans of (newlines, matching lines) over the tile's
@@ -984,10 +1098,21 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
               w0 = w.x;
               w1 = w.y;
             }
+            // kSlotLong: the lane's last line, whose length (or pending
+            // index) the lane kept in its tails entry
+            uint64_t len = w1 & kSlotLong;
+            uint32_t flags = (w1 & kCandidateBit) ? kMetaCand : 0u;
+            if (len == kSlotLong) {
+              len = tails[k];
+              if (len & kTailPending) {
+                len &= ~kTailPending;
+                flags |= kMetaPend;
+              }
+            }
             StagedLine L;
             L.start = cs[k] + (w0 & 0xffffu);
-            L.len = w1;
-            L.rel = nl_off[k] + (w0 >> 16);
+            L.len_lo = uint32_t(len);
+            L.meta = (nl_off[k] + (w0 >> 16)) | flags | (flags & kMetaPend ? 0u : uint32_t(len >> 32) << 24);
             a.staging[o] = L;
           }
         }
@@ -1085,9 +1210,15 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
       if (k < ti.count && src < v.staging_cap) {
         L = v.staging[src];
         keep = true;
-        if (L.len & kCandidateBit) {
-          L.len &= ~kCandidateBit;
-          keep = line_matches(L.start, L.start + L.len);
+        if (L.meta & kMetaPend) {
+          // a long line parked by the scan, resolved from the chunk maps
+          const PendingLine P = v.pend[L.len_lo];
+          keep = P.matched != 0u;
+          L.len_lo = uint32_t(P.len);
+          L.meta = staged_rel(L) | (uint32_t(P.len >> 32) << 24);
+        } else if (L.meta & kMetaCand) {
+          L.meta &= ~kMetaCand;
+          keep = line_matches(L.start, L.start + staged_len(L));
         }
       }
       const uint64_t m = __ballot(keep);
@@ -1276,6 +1407,155 @@ __device__ __forceinline__ bool nfa_line_matches(const NfaView& g, const uint8_t
   return m;
 }
 
+// The staged lines of a scan with PENDING lines and no filter candidates: only
+// the pending ones change (kept iff they match; length filled in).
+__global__ __launch_bounds__(256) void resolve_tiles_kernel(VerifyArgs v) {
+  verify_tiles(v, [](uint64_t, uint64_t) { return true; });
+}
+
+// ---- long lines -------------------------------------------------------------
+// A line the scan parked (park_pending) is finished here, in parallel over its
+// bytes instead of by one lane: long_end_kernel finds its end ('\n' or the
+// split's end) from the per-chunk '\n' counts; the host cuts [resume, end) into
+// segments; long_map_kernel computes each segment's transition map (every
+// state at once: each lane the map of its 1/64 of the segment, then the wave
+// composes the 64 maps in order); long_fin_kernel applies a line's segment maps
+// in order to its parked state, and the line matches iff '\n' then enters
+// start_m (the DFA's own rule, also for the split's unterminated last line).
+// States are the blob's (u8 table [S][256], S <= 256).
+
+// one wave per parked line
+__global__ __launch_bounds__(256) void long_end_kernel(LongArgs la) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t waves = uint64_t(gridDim.x) * 4;
+  for (uint64_t i = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); i < la.npend; i += waves) {
+    PendingLine P = la.pend[i];
+    uint64_t c = P.resume / la.chunk, end = la.n;
+    for (;; c += 64) {
+      const uint64_t cc = c + lane;
+      const bool past = cc >= la.nchunks;
+      const uint64_t hit = __ballot(past || la.chunk_nl[cc < la.nchunks ? cc : 0] != 0u);
+      if (!hit) continue;
+      const uint64_t ch = c + uint64_t(__builtin_ctzll(hit));
+      if (ch < la.nchunks) {
+        // the first '\n' of chunk ch: 64 lanes x 16 B per round
+        const uint64_t cb = ch * la.chunk, ce = cb + la.chunk < la.n ? cb + la.chunk : la.n;
+        for (uint64_t q0 = cb; q0 < ce; q0 += 1024) {
+          const uint64_t q = q0 + 16u * lane;
+          uint32_t first = 0xffffffffu;
+          if (q < ce) {
+            uint4 v;
+            if (q + 16 <= la.n) {
+              v = *reinterpret_cast<const uint4*>(la.data + q);
+            } else {
+              uint32_t w[4] = {0, 0, 0, 0};
+              for (uint64_t b = q; b < la.n; ++b) w[(b - q) >> 2] |= uint32_t(la.data[b]) << (8 * ((b - q) & 3));
+              v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+            for (int k = 3; k >= 0; --k) {
+              const uint32_t m = nl_mask(ws[k]);
+              if (m && q + 4u * uint32_t(k) + (uint32_t(__builtin_ctz(m)) >> 3) < ce)
+                first = 4u * uint32_t(k) + (uint32_t(__builtin_ctz(m)) >> 3);
+            }
+          }
+          const uint64_t h2 = __ballot(first != 0xffffffffu);
+          if (h2) {
+            const int l = __builtin_ctzll(h2);
+            end = q0 + 16u * uint32_t(l) + uint32_t(__shfl(int(first), l, 64));
+            break;
+          }
+        }
+      }
+      break;
+    }
+    if (lane == 0) {
+      P.end = end;
+      la.pend[i] = P;
+    }
+  }
+}
+
+// one wave per segment; the map of a piece is computed with every DFA state at
+// once: S <= 8 as Sheng byte vectors (8 next states per input byte, two v_perm
+// per byte), else one map of S bytes per lane in LDS
+constexpr int kLongWaves = 1;  // waves per workgroup of long_map_kernel (its LDS holds one [S][256] table)
+__global__ __launch_bounds__(64 * kLongWaves) void long_map_kernel(LongArgs la) {
+  __shared__ __attribute__((aligned(16))) uint8_t tbl[256 * 256];
+  __shared__ __attribute__((aligned(16))) uint8_t maps[64 * kLongWaves * 256];
+  __shared__ uint2 v8[256];  // S <= 8: V[b] = the 8 next states of byte b
+  const uint32_t S = la.nstates, lane = threadIdx.x & 63u;
+  for (uint32_t i = threadIdx.x * 16u; i < S * 256u; i += 64u * kLongWaves * 16u)
+    *reinterpret_cast<uint4*>(tbl + i) = *reinterpret_cast<const uint4*>(la.tbl + i);
+  __syncthreads();
+  if (S <= 8) {
+    for (uint32_t b = threadIdx.x; b < 256; b += 64u * kLongWaves) {
+      uint32_t vx = 0, vy = 0;
+      for (uint32_t s = 0; s < 4; ++s) {
+        vx |= uint32_t(tbl[(s < S ? s : 0) * 256u + b]) << (8 * s);
+        vy |= uint32_t(tbl[(s + 4 < S ? s + 4 : 0) * 256u + b]) << (8 * s);
+      }
+      v8[b] = make_uint2(vx, vy);
+    }
+    __syncthreads();
+  }
+  uint8_t* my = maps + threadIdx.x * 256u;
+  const uint64_t waves = uint64_t(gridDim.x) * kLongWaves;
+  for (uint64_t g = uint64_t(blockIdx.x) * kLongWaves + (threadIdx.x >> 6); g < la.nseg; g += waves) {
+    const LongSeg sg = la.seg[g];
+    // this lane's piece: [a, e), 16-aligned cuts
+    const uint64_t span = sg.end - sg.begin;
+    const uint64_t per = ((span + 63) / 64 + 15) & ~uint64_t(15);
+    const uint64_t a = sg.begin + per * lane < sg.end ? sg.begin + per * lane : sg.end;
+    const uint64_t e = a + per < sg.end ? a + per : sg.end;
+    uint8_t* out = la.segmap + g * 256u;
+    if (S <= 8) {
+      uint32_t lo = 0x03020100u, hi = 0x07060504u;
+      for_line_bytes(la.data, a, e, [&](uint32_t b) {
+        const uint2 v = v8[b];
+        lo = __builtin_amdgcn_perm(v.y, v.x, lo);
+        hi = __builtin_amdgcn_perm(v.y, v.x, hi);
+        return true;
+      });
+      // compose the 64 lane maps in lane (= byte) order
+      uint32_t alo = 0x03020100u, ahi = 0x07060504u;
+      for (int l = 0; l < 64; ++l) {
+        const uint32_t ml = __shfl(lo, l, 64), mh = __shfl(hi, l, 64);
+        alo = __builtin_amdgcn_perm(mh, ml, alo);
+        ahi = __builtin_amdgcn_perm(mh, ml, ahi);
+      }
+      if (lane < 8u) out[lane] = uint8_t((lane < 4 ? alo >> (8 * lane) : ahi >> (8 * (lane - 4))) & 0xffu);
+    } else {
+      for (uint32_t s = 0; s < S; ++s) my[s] = uint8_t(s);
+      for_line_bytes(la.data, a, e, [&](uint32_t b) {
+        for (uint32_t s = 0; s < S; ++s) my[s] = tbl[uint32_t(my[s]) * 256u + b];
+        return true;
+      });
+      __builtin_amdgcn_wave_barrier();
+      // lane j follows states j, j + 64, ... through the 64 lane maps in order
+      uint8_t* wm = maps + (threadIdx.x & ~63u) * 256u;
+      for (uint32_t s = lane; s < S; s += 64) {
+        uint32_t x = s;
+        for (int l = 0; l < 64; ++l) x = wm[uint32_t(l) * 256u + x];
+        out[s] = uint8_t(x);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// one lane per parked line
+__global__ __launch_bounds__(256) void long_fin_kernel(LongArgs la) {
+  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < la.npend; i += uint64_t(gridDim.x) * 256) {
+    PendingLine P = la.pend[i];
+    uint32_t s = la.st2id[P.state];
+    for (uint64_t g = la.seg_off[i]; g < la.seg_off[i + 1]; ++g) s = la.segmap[g * 256u + s];
+    P.matched = la.tbl[s * 256u + uint32_t('\n')] == la.start_m ? 1u : 0u;
+    P.len = P.end - P.line_start;
+    la.pend[i] = P;
+  }
+}
+
 __global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
   const NfaView g = nfa_view(v.nfa);
   verify_tiles(v, [&](uint64_t a, uint64_t e) { return nfa_line_matches(g, v.data, a, e); });
@@ -1366,7 +1646,7 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
                                                           uint64_t ntiles, const uint64_t* out_off,
                                                           const uint64_t* line_base, uint64_t staging_cap,
                                                           uint64_t capacity, uint64_t* line_no, uint64_t* start,
-                                                          uint32_t* len) {
+                                                          uint64_t* len) {
   const uint64_t waves = uint64_t(gridDim.x) * 4;
   for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles; t += waves) {
     const TileInfo ti = tiles[t];
@@ -1376,9 +1656,9 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
       const uint64_t src = ti.base + k, dst = o + k;
       if (src < staging_cap && dst < capacity) {
         const StagedLine L = staging[src];
-        line_no[dst] = lb + L.rel;
+        line_no[dst] = lb + staged_rel(L);
         start[dst] = L.start;
-        len[dst] = L.len;
+        len[dst] = staged_len(L);
       }
     }
   }
@@ -1534,7 +1814,7 @@ uint64_t order_blocks(uint64_t ntiles) { return (ntiles + kOrdTiles - 1) / kOrdT
 // out_off / line_base: ntiles entries; blk: 2 * order_blocks(ntiles) scratch
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
                        uint64_t* line_base, uint64_t* blk, uint64_t staging_cap, uint64_t capacity,
-                       uint64_t* line_no, uint64_t* start, uint32_t* len, hipStream_t stream) {
+                       uint64_t* line_no, uint64_t* start, uint64_t* len, hipStream_t stream) {
   const uint64_t nblk = order_blocks(ntiles);
   uint64_t* blk_cnt = blk;
   uint64_t* blk_nl = blk + nblk;
@@ -1551,11 +1831,32 @@ hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_
 
 uint32_t verify_hot_bytes() { return kVerifyHotBytes; }
 
-hipError_t verify_candidates(const VerifyArgs& v, hipStream_t stream) {
+hipError_t long_lines_end(const LongArgs& la, hipStream_t stream) {
+  uint64_t grid = (la.npend + 3) / 4;
+  if (grid > 16384) grid = 16384;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(long_end_kernel, dim3(grid), dim3(256), 0, stream, la);
+  return hipGetLastError();
+}
+hipError_t long_lines_resolve(const LongArgs& la, hipStream_t stream) {
+  if (la.nseg) {
+    uint64_t grid = (la.nseg + kLongWaves - 1) / kLongWaves;
+    if (grid > 65536) grid = 65536;
+    hipLaunchKernelGGL(long_map_kernel, dim3(grid), dim3(64 * kLongWaves), 0, stream, la);
+  }
+  uint64_t grid = (la.npend + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  if (grid) hipLaunchKernelGGL(long_fin_kernel, dim3(grid), dim3(256), 0, stream, la);
+  return hipGetLastError();
+}
+
+hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t stream) {
   uint64_t grid = (v.ntiles + 3) / 4;
   if (grid > 16384) grid = 16384;
   if (grid == 0) return hipSuccess;
-  if (v.nfa)
+  if (!candidates)
+    hipLaunchKernelGGL(resolve_tiles_kernel, dim3(grid), dim3(256), 0, stream, v);
+  else if (v.nfa)
     hipLaunchKernelGGL(verify_nfa_kernel, dim3(grid), dim3(256), 0, stream, v);
   else if (v.full_u32)
     hipLaunchKernelGGL(verify_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, v);

@@ -8,9 +8,15 @@
 // DEBUG 15 %, WARN 10 %, ERROR 5 %; the lowercase word "error" is planted in
 // 2 % of messages and the phrase "timeout while waiting for lock" in 0.5 %.
 // kind 1 additionally plants one of the seed's 1,000 keywords (a-z, 5-12
-// letters, random letter case) in 1 % of messages (config 4). Bytes are
-// printable ASCII plus '\n'. Any page can be regenerated alone, so a window of
-// a 16 GiB split can be checked on the CPU.
+// letters, random letter case) in 1 % of messages (config 4). kind 2 is a
+// long-line corpus: a page is a "boundary" page (normal log lines, as kind 0)
+// with probability 1/512, else filler -- space-separated words, no '\n', the
+// word "error" in 1 page of 2048 -- so lines of consecutive filler pages,
+// 4 MiB long on average (geometric), alternate with a page of short lines;
+// kind 3 is kind 2 whose first 1 GiB holds no boundary page (one newline-free
+// line of 1 GiB plus the head of the next boundary page). Bytes are printable
+// ASCII plus '\n'. Any page can be regenerated alone, so a window of a 16 GiB
+// split can be checked on the CPU.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -126,8 +132,35 @@ DG_HD void line(uint64_t seed, uint64_t page, uint32_t li, int kind, char* o, ui
   o[end] = '\n';
 }
 
+// kinds 2 / 3: a filler page of a long line (no '\n')
+DG_HD void filler_page(uint64_t seed, uint64_t page, char* o, uint32_t bytes) {
+  Rng r{mix(seed + 0xf111) ^ mix(page)};
+  const bool plant = r.below(2048) == 0;
+  const uint32_t at = r.below(bytes > 8 ? bytes - 8 : 1);
+  uint32_t p = 0;
+  while (p < bytes) {
+    int wl;
+    const char* wd = word(r.below(32), &wl);
+    for (int k = 0; k < wl && p < bytes; ++k) o[p++] = wd[k];
+    if (p < bytes) o[p++] = ' ';
+  }
+  if (plant)
+    for (int k = 0; k < 5 && at + uint32_t(k) < bytes; ++k) o[at + k] = "error"[k];
+}
+constexpr uint32_t kLongBoundary = 512;          // 1 page in 512 ends a long line
+constexpr uint64_t kLongFirstPages = (1u << 30) / kPage;  // kind 3: first 1 GiB
+
 // Fills page `page` (kPage bytes, or fewer for the split's last page: `bytes`).
 DG_HD void page_fill(uint64_t seed, uint64_t page, int kind, char* o, uint32_t bytes) {
+  if (kind == 2 || kind == 3) {
+    const bool boundary = (mix(seed ^ 0xb0b0) ^ mix(page + 7)) % kLongBoundary == 0 &&
+                          !(kind == 3 && page < kLongFirstPages);
+    if (!boundary) {
+      filler_page(seed, page, o, bytes);
+      return;
+    }
+    kind = 0;
+  }
   Rng r{mix(seed + 0x5151) ^ mix(page)};
   uint32_t p = 0, li = 0;
   while (p < bytes) {

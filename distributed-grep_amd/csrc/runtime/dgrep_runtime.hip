@@ -52,8 +52,10 @@ hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStr
 uint64_t order_blocks(uint64_t ntiles);
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
                        uint64_t* line_base, uint64_t* blk, uint64_t staging_cap, uint64_t capacity,
-                       uint64_t* line_no, uint64_t* start, uint32_t* len, hipStream_t stream);
-hipError_t verify_candidates(const VerifyArgs& v, hipStream_t stream);
+                       uint64_t* line_no, uint64_t* start, uint64_t* len, hipStream_t stream);
+hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t stream);
+hipError_t long_lines_end(const LongArgs& la, hipStream_t stream);
+hipError_t long_lines_resolve(const LongArgs& la, hipStream_t stream);
 uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
@@ -111,13 +113,30 @@ struct dgrep_ctx {
   uint64_t overflow_cap = 0;
   uint2* d_spill = nullptr;  // HBM spill areas of the resident threads (ScanArgs::spill)
   uint64_t spill_cap = 0;
+  uint64_t* d_tails = nullptr;     // ScanArgs::tails (resident threads x streams)
+  uint64_t tails_cap = 0;
+  uint32_t* d_chunk_nl = nullptr;  // '\n' per chunk (ScanArgs::chunk_nl)
+  uint64_t chunk_nl_cap = 0;
+  PendingLine* d_pend = nullptr;   // parked long lines
+  uint64_t pend_cap = 0;
+  // long lines: the blob's u8 [S][256] table and stepper state -> blob state
+  // (only for <= 256-state DFAs on the Sheng / pair / table steppers)
+  uint8_t* d_long_tbl = nullptr;
+  uint32_t* d_st2id = nullptr;
+  uint32_t long_start_m = 0, long_states = 0;
+  LongSeg* d_seg = nullptr;
+  uint64_t seg_cap = 0;
+  uint64_t* d_seg_off = nullptr;
+  uint64_t seg_off_cap = 0;
+  uint8_t* d_segmap = nullptr;
+  uint64_t segmap_cap = 0;
 
   // dgrep_scan (host data) buffers
   uint8_t* d_data = nullptr;
   size_t data_cap = 0;
   uint64_t* d_res_line = nullptr;
   uint64_t* d_res_start = nullptr;
-  uint32_t* d_res_len = nullptr;
+  uint64_t* d_res_len = nullptr;
   uint64_t res_cap = 0;
 
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr;
@@ -193,7 +212,7 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 // start_m, then shadow(start_m): a pair-end id >= first shadow holds an
 // event. Returns false if the DFA does not fit (T2 > kPairMaxT2 bytes).
 bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::vector<uint8_t>* img, uint32_t* start,
-                      uint32_t* start_m, PairArgs* pa) {
+                      uint32_t* start_m, PairArgs* pa, std::vector<uint32_t>* orig_out) {
   const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
   const uint32_t cn = h.byte_class[uint8_t('\n')];
   auto T = [&](uint32_t s, uint32_t c) { return trans[size_t(s) * K + c]; };
@@ -251,6 +270,7 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   }
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
+  *orig_out = orig;  // pair state index -> blob state (a shadow -> the state it copies)
   pa->t1 = uint32_t(t1_off);
   pa->thr = premul(thr_id);
   pa->div = uint32_t(row);
@@ -371,7 +391,8 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl,
+                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -447,8 +468,9 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   }
   std::vector<uint8_t> pair_img;
   uint32_t pair_start = 0, pair_m = 0;
+  std::vector<uint32_t> st2id;  // stepper state index -> blob state (long lines, see resolve_long_lines)
   const bool pair_ok = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3)
-                           ? build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args)
+                           ? build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args, &st2id)
                            : false;
   if (force == 3 && !pair_ok) {
     c->err = "dgrep_load_dfa: the pair stepper's two-byte table does not fit this DFA";
@@ -581,10 +603,14 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
         t[size_t(b) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
     start = id[h.start] * 0x01010101u;
     start_m = top;
+    st2id.assign(S, 0);
+    for (uint32_t x = 0; x < S; ++x) st2id[id[x]] = x;
   } else {
     // StepTable: row s (stride scan_table_row() = 260, bank-staggered) holds
     // trans[s][class(b)] at byte b
     c->step_kind = kStepTable;
+    st2id.resize(h.nstates);
+    for (uint32_t x = 0; x < h.nstates; ++x) st2id[x] = x;
     const size_t row = scan_table_row();
     t.assign((size_t(h.nstates) * row + 15) & ~size_t(15), 0);
     for (uint32_t s = 0; s < h.nstates; ++s)
@@ -605,6 +631,24 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->nstates = h.nstates;
   c->start = start;
   c->start_m = start_m;
+  // long lines: the blob's u8 [S][256] table for the long-line kernels
+  if (c->d_long_tbl) HIPCHK(hipFree(c->d_long_tbl));
+  if (c->d_st2id) HIPCHK(hipFree(c->d_st2id));
+  c->d_long_tbl = nullptr;
+  c->d_st2id = nullptr;
+  c->long_states = 0;
+  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepTable) && h.nstates <= 256 &&
+      !st2id.empty()) {
+    std::vector<uint8_t> lt(size_t(h.nstates) * 256);
+    for (uint32_t s = 0; s < h.nstates; ++s)
+      for (int b = 0; b < 256; ++b) lt[size_t(s) * 256 + b] = uint8_t(trans[size_t(s) * h.nclasses + h.byte_class[b]]);
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_long_tbl), lt.size()));
+    HIPCHK(hipMemcpy(c->d_long_tbl, lt.data(), lt.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_st2id), st2id.size() * 4));
+    HIPCHK(hipMemcpy(c->d_st2id, st2id.data(), st2id.size() * 4, hipMemcpyHostToDevice));
+    c->long_states = h.nstates;
+    c->long_start_m = h.start_m;
+  }
   c->empty_line_matches = trans[size_t(h.start) * h.nclasses + h.byte_class[uint8_t('\n')]] == h.start_m;
   int bpc = 0;
   HIPCHK(scan_dfa_occupancy(c->step_kind, c->table_bytes, &bpc));
@@ -615,10 +659,60 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   return DGREP_OK;
 }
 
+// The lines the scan parked (npend > 0): their ends, then their segments'
+// maps, then each line's verdict and length (long_* kernels in scan_dfa.hip).
+// The segment cut is made on the host from the ends (one small readback).
+static int resolve_long_lines(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64_t chunk, uint64_t nchunks,
+                              uint64_t npend) {
+  int rc;
+  LongArgs la;
+  memset(&la, 0, sizeof la);
+  la.data = d_data;
+  la.n = n;
+  la.chunk = chunk;
+  la.nchunks = nchunks;
+  la.chunk_nl = c->d_chunk_nl;
+  la.pend = c->d_pend;
+  la.npend = npend;
+  la.st2id = c->d_st2id;
+  la.tbl = c->d_long_tbl;
+  la.nstates = c->long_states;
+  la.start_m = c->long_start_m;
+  HIPCHK(long_lines_end(la, c->stream));
+  std::vector<PendingLine> P(npend);
+  HIPCHK(hipMemcpyAsync(P.data(), c->d_pend, npend * sizeof(PendingLine), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  // segments of about 1/4096 of the parked bytes (so the GPU fills), at least
+  // 256 KiB (a wave's 64 pieces of 4 KiB) and 64-B aligned
+  uint64_t total = 0;
+  for (const PendingLine& p : P) total += p.end > p.resume ? p.end - p.resume : 0;
+  uint64_t seg = std::max<uint64_t>(uint64_t(256) << 10, (total / 4096 + 63) & ~uint64_t(63));
+  std::vector<LongSeg> segs;
+  std::vector<uint64_t> off(npend + 1, 0);
+  for (uint64_t i = 0; i < npend; ++i) {
+    for (uint64_t b = P[i].resume; b < P[i].end; b += seg) segs.push_back(LongSeg{b, std::min(P[i].end, b + seg)});
+    off[i + 1] = segs.size();
+  }
+  if ((rc = grow(c, &c->d_seg, &c->seg_cap, std::max<uint64_t>(segs.size(), 1))) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_seg_off, &c->seg_off_cap, npend + 1)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_segmap, &c->segmap_cap, std::max<uint64_t>(segs.size(), 1) * 256)) != DGREP_OK) return rc;
+  if (!segs.empty())
+    HIPCHK(hipMemcpyAsync(c->d_seg, segs.data(), segs.size() * sizeof(LongSeg), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_seg_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, c->stream));
+  la.seg = c->d_seg;
+  la.nseg = segs.size();
+  la.seg_off = c->d_seg_off;
+  la.segmap = c->d_segmap;
+  HIPCHK(long_lines_resolve(la, c->stream));
+  // the host vectors are read by the async copies above: wait before they go
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return DGREP_OK;
+}
+
 // Core of every scan: the split is resident at d_data (n bytes). Results go to
 // device arrays of `capacity` lines; *count receives the number of matches.
 static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64_t* d_line, uint64_t* d_start,
-                         uint32_t* d_len, uint64_t capacity, uint64_t* count) {
+                         uint64_t* d_len, uint64_t capacity, uint64_t* count) {
   *count = 0;
   dgrep_scan_stats& S = c->stats;
   S = dgrep_scan_stats{};
@@ -632,10 +726,9 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     S.matches = 1;
     if (capacity >= 1) {
       const uint64_t one = 1, zero = 0;
-      const uint32_t zl = 0;
       HIPCHK(hipMemcpyAsync(d_line, &one, 8, hipMemcpyHostToDevice, c->stream));
       HIPCHK(hipMemcpyAsync(d_start, &zero, 8, hipMemcpyHostToDevice, c->stream));
-      HIPCHK(hipMemcpyAsync(d_len, &zl, 4, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(d_len, &zero, 8, hipMemcpyHostToDevice, c->stream));
       HIPCHK(hipStreamSynchronize(c->stream));
     }
     return DGREP_OK;
@@ -667,6 +760,17 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   if (use_spill &&
       (rc = grow(c, &c->d_spill, &c->spill_cap, uint64_t(grid) * threads * DGREP_SPILL_RECORDS)) != DGREP_OK)
     return rc;
+  // long lines: the lanes' tail entries, '\n' per chunk and the pending list
+  // (parking needs the blob's table: <= 256-state DFAs on the Sheng / pair /
+  // table steppers)
+  const uint32_t streams = tile / (uint64_t(kTileLanes) * chunk);
+  if ((rc = grow(c, &c->d_tails, &c->tails_cap, uint64_t(grid) * threads * streams)) != DGREP_OK) return rc;
+  const bool park = c->d_long_tbl != nullptr;
+  const uint64_t nchunks = (n + chunk - 1) / chunk;
+  if (park) {
+    if ((rc = grow(c, &c->d_chunk_nl, &c->chunk_nl_cap, nchunks)) != DGREP_OK) return rc;
+    if (!c->d_pend && (rc = grow(c, &c->d_pend, &c->pend_cap, 1024)) != DGREP_OK) return rc;
+  }
 
   ScanArgs a;
   memset(&a, 0, sizeof a);
@@ -680,8 +784,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.ntiles = ntiles;
   a.counter = c->d_counters;
   a.tiles = c->d_tiles;
-  a.status = reinterpret_cast<uint32_t*>(c->d_counters + 2);
   a.overflow_count = c->d_counters + 1;
+  a.pend_count = c->d_counters + 2;
+  a.tails = c->d_tails;
+  a.chunk_nl = park ? c->d_chunk_nl : nullptr;
   a.wide = c->d_wide;
   a.nclasses = c->nclasses;
   a.hot_entries = c->hot_entries;
@@ -705,6 +811,8 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     a.capacity = c->staging_cap;
     a.overflow = c->d_overflow;
     a.overflow_cap = c->overflow_cap;
+    a.pend = park ? c->d_pend : nullptr;
+    a.pend_cap = park ? c->pend_cap : 0;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     HIPCHK(scan_dfa(c->step_kind, a, grid, c->stream));
@@ -718,6 +826,9 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     if (ctr[1] > c->overflow_cap) {
       // more overflowing lanes than recorded: grow the list and scan again
       if ((rc = grow(c, &c->d_overflow, &c->overflow_cap, ctr[1])) != DGREP_OK) return rc;
+    } else if (park && ctr[2] > c->pend_cap) {
+      // more parked long lines than the pending list holds
+      if ((rc = grow(c, &c->d_pend, &c->pend_cap, ctr[2])) != DGREP_OK) return rc;
     } else if (filt && ctr[0] > c->staging_cap) {
       // candidates included, more staged lines than the staging buffer holds
       if ((rc = grow(c, &c->d_staging, &c->staging_cap, ctr[0] + ctr[0] / 8)) != DGREP_OK) return rc;
@@ -726,16 +837,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     }
   }
   const uint64_t staged = ctr[0];
+  const uint64_t npend = park ? ctr[2] : 0;
   S.overflow_lanes = ctr[1];
+  S.pending = npend;
   c->last_ms = S.scan_ms;
-  if (uint32_t(ctr[2]) & kStatusLineTooLong) {
-    c->err = "a matching line is longer than 4 GiB (uint32 length in dgrep_result)";
-    return DGREP_E_UNSUPPORTED;
-  }
-  if (uint32_t(ctr[2]) & kStatusCandidateTooLong) {
-    c->err = "a line that leaves the filter's LDS-resident states is longer than 2 GiB";
-    return DGREP_E_UNSUPPORTED;
-  }
   // matching (and candidate) lines per byte: caps the next scan's lane chunk
   c->density = double(staged) / double(n);
   const bool over = ctr[1] && staged <= a.capacity;
@@ -745,7 +850,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     HIPCHK(hipEventRecord(c->ev3, c->stream));
   }
   uint64_t total = staged;
-  if (filt && staged && staged <= a.capacity) {
+  if ((filt || npend) && staged && staged <= a.capacity) {
     VerifyArgs v;
     v.data = d_data;
     v.full = c->d_full;
@@ -762,8 +867,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.removed = c->d_counters + 3;  // zeroed before the scan
     v.nfa = c->d_nfa;
     v.matched = c->d_nfa ? UINT32_MAX : c->blob_matched;
+    v.pend = c->d_pend;
     HIPCHK(hipEventRecord(c->ev4, c->stream));
-    HIPCHK(verify_candidates(v, c->stream));
+    if (npend && (rc = resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) return rc;
+    HIPCHK(verify_candidates(v, filt, c->stream));
     HIPCHK(hipEventRecord(c->ev5, c->stream));
     unsigned long long removed = 0;
     HIPCHK(hipMemcpyAsync(&removed, c->d_counters + 3, 8, hipMemcpyDeviceToHost, c->stream));
@@ -788,7 +895,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
 }
 
 extern "C" int dgrep_scan_device(dgrep_ctx* c, const void* d_data, size_t n, uint64_t* d_line_no, uint64_t* d_start,
-                                 uint32_t* d_len, uint64_t capacity, uint64_t* count) {
+                                 uint64_t* d_len, uint64_t capacity, uint64_t* count) {
   if (!c || !count || (n && !d_data)) return DGREP_E_INVALID;
   if (!c->loaded) { c->err = "no DFA loaded"; return DGREP_E_NO_DFA; }
   HIPCHK(hipSetDevice(c->device));
@@ -919,21 +1026,21 @@ extern "C" int dgrep_scan(dgrep_ctx* c, const uint8_t* data, size_t n, dgrep_res
   if (count == 0) return DGREP_OK;
   out->line_no = static_cast<uint64_t*>(malloc(count * 8));
   out->start = static_cast<uint64_t*>(malloc(count * 8));
-  out->len = static_cast<uint32_t*>(malloc(count * 4));
+  out->len = static_cast<uint64_t*>(malloc(count * 8));
   if (!out->line_no || !out->start || !out->len) {
     dgrep_result_free(out);
     return DGREP_E_NOMEM;
   }
   HIPCHK(hipMemcpyAsync(out->line_no, c->d_res_line, count * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(out->start, c->d_res_start, count * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(out->len, c->d_res_len, count * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out->len, c->d_res_len, count * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return DGREP_OK;
 }
 
 // ---- partition + intermediate writer (map_reduce/worker.go:13-17,78-109) ----
 static int encode_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, const uint64_t* d_line, const uint64_t* d_start,
-                           const uint32_t* d_len, uint64_t count, const char* filename, size_t fn, uint32_t nreduce,
+                           const uint64_t* d_len, uint64_t count, const char* filename, size_t fn, uint32_t nreduce,
                            uint8_t* d_out, uint64_t out_cap, uint64_t* begin, uint64_t* end, uint64_t* total) {
   if (nreduce == 0 || nreduce > 65535) { c->err = "nreduce must be 1..65535"; return DGREP_E_INVALID; }
   if (count >= (uint64_t(1) << 32)) { c->err = "more than 2^32-1 records"; return DGREP_E_UNSUPPORTED; }
@@ -977,7 +1084,7 @@ static int encode_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, cons
 }
 
 extern "C" int dgrep_encode_device(dgrep_ctx* c, const void* d_data, size_t n, const uint64_t* d_line_no,
-                                   const uint64_t* d_start, const uint32_t* d_len, uint64_t count,
+                                   const uint64_t* d_start, const uint64_t* d_len, uint64_t count,
                                    const char* filename, size_t fn, uint32_t nreduce, void* d_out, uint64_t out_cap,
                                    uint64_t* part_begin, uint64_t* part_end, uint64_t* total) {
   if (!c || !part_begin || !part_end || !total || (fn && !filename) || (count && (!d_line_no || !d_start || !d_len)) ||

@@ -74,7 +74,7 @@ class UnsupportedPattern(DgrepError):
 
 class _Result(ctypes.Structure):
     _fields_ = [("count", ctypes.c_uint64), ("line_no", ctypes.POINTER(ctypes.c_uint64)),
-                ("start", ctypes.POINTER(ctypes.c_uint64)), ("len", ctypes.POINTER(ctypes.c_uint32))]
+                ("start", ctypes.POINTER(ctypes.c_uint64)), ("len", ctypes.POINTER(ctypes.c_uint64))]
 
 
 class _Partitions(ctypes.Structure):
@@ -90,7 +90,7 @@ class _ScanStats(ctypes.Structure):
     _fields_ = [("stepper", ctypes.c_uint32), ("lane_chunk", ctypes.c_uint32), ("lane_slots", ctypes.c_uint32),
                 ("scan_attempts", ctypes.c_uint32), ("tiles", ctypes.c_uint64), ("overflow_lanes", ctypes.c_uint64),
                 ("matches", ctypes.c_uint64), ("scan_ms", ctypes.c_float), ("overflow_ms", ctypes.c_float),
-                ("verify_ms", ctypes.c_float), ("candidates", ctypes.c_uint64)]
+                ("verify_ms", ctypes.c_float), ("candidates", ctypes.c_uint64), ("pending", ctypes.c_uint64)]
 
 
 class _BlobInfo(ctypes.Structure):
@@ -293,7 +293,7 @@ class Context:
         return cp
 
     def scan(self, contents) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-        """Host split -> (line_no u64[], start u64[], len u32[]) of matching lines."""
+        """Host split -> (line_no u64[], start u64[], len u64[]) of matching lines."""
         if isinstance(contents, str):
             contents = contents.encode("utf-8", "surrogateescape")
         buf = np.frombuffer(contents, dtype=np.uint8) if len(contents) else np.zeros(1, np.uint8)
@@ -302,7 +302,7 @@ class Context:
         try:
             n = int(res.count)
             if n == 0:
-                return np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint32)
+                return np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint64)
             ln = np.ctypeslib.as_array(res.line_no, shape=(n,)).copy()
             st = np.ctypeslib.as_array(res.start, shape=(n,)).copy()
             le = np.ctypeslib.as_array(res.len, shape=(n,)).copy()

@@ -58,12 +58,13 @@ typedef struct dgrep_ctx dgrep_ctx;
 
 /* Matching lines of one split, ascending line order (grep.go:20 iteration
  * order). line_no is 1-based (grep.go:25 `line_number+1`); start/len index
- * the split's bytes; the line excludes its '\n' (strings.Split). */
+ * the split's bytes; the line excludes its '\n' (strings.Split). len is 64-bit:
+ * a Go string (and so a line of one) may be longer than 4 GiB. */
 typedef struct {
   uint64_t count;
   uint64_t* line_no;
   uint64_t* start;
-  uint32_t* len;
+  uint64_t* len;
 } dgrep_result;
 
 typedef struct {
@@ -171,7 +172,7 @@ void dgrep_partitions_free(dgrep_partitions* p);
  * bytes; *total receives the bytes needed -- if larger, call again with a
  * bigger buffer); part_begin/part_end are host arrays of nreduce entries. */
 int dgrep_encode_device(dgrep_ctx* ctx, const void* d_data, size_t n, const uint64_t* d_line_no,
-                        const uint64_t* d_start, const uint32_t* d_len, uint64_t count, const char* filename,
+                        const uint64_t* d_start, const uint64_t* d_len, uint64_t count, const char* filename,
                         size_t fn, uint32_t nreduce, void* d_out, uint64_t out_cap, uint64_t* part_begin,
                         uint64_t* part_end, uint64_t* total);
 /* Device time (ms) of the last encode (HIP events on the context stream). */
@@ -200,7 +201,7 @@ void dgrep_reduce_free(dgrep_reduce_out* r);
  * written: call again with a larger capacity). Asynchronous on the context
  * stream except for the 8-byte count readback. */
 int dgrep_scan_device(dgrep_ctx* ctx, const void* d_data, size_t n, uint64_t* d_line_no, uint64_t* d_start,
-                      uint32_t* d_len, uint64_t capacity, uint64_t* count);
+                      uint64_t* d_len, uint64_t capacity, uint64_t* count);
 
 /* ---- bench / test tooling ------------------------------------------------ */
 /* Fill d_out[0:n) with the seeded synthetic log corpus on
@@ -228,8 +229,10 @@ typedef struct {
   uint64_t matches;        /* matching lines */
   float scan_ms;           /* scan kernel, all attempts */
   float overflow_ms;       /* overflow pass */
-  float verify_ms;         /* filter stepper: re-run of the candidate lines on the whole DFA */
+  float verify_ms;         /* filter stepper: re-run of the candidate lines on the whole DFA; Sheng: resolution
+                              of the parked long lines */
   uint64_t candidates;     /* filter stepper: candidate lines dropped by that re-run */
+  uint64_t pending;        /* Sheng: long lines parked by the scan and resolved from chunk maps */
 } dgrep_scan_stats;
 int dgrep_last_scan_stats(dgrep_ctx* ctx, dgrep_scan_stats* out);
 

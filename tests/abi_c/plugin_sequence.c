@@ -65,7 +65,8 @@ static void* scan_thread(void* p) {
 static void dump(FILE* out, const dgrep_result* r) {
   fprintf(out, "# %llu\n", (unsigned long long)r->count);
   for (uint64_t i = 0; i < r->count; ++i)
-    fprintf(out, "%llu %llu %u\n", (unsigned long long)r->line_no[i], (unsigned long long)r->start[i], r->len[i]);
+    fprintf(out, "%llu %llu %llu\n", (unsigned long long)r->line_no[i], (unsigned long long)r->start[i],
+            (unsigned long long)r->len[i]);
 }
 
 int main(int argc, char** argv) {

@@ -84,3 +84,20 @@ def test_build_info_names_commit_and_arch():
     head = info.split()[0]
     assert re.fullmatch(r"head=([0-9a-f]{40}(-dirty)?|unknown)", head), info
     assert "arch=gfx950" in info and "hipflags=" in info
+
+
+def test_synth_long_line_kinds():
+    """kinds 2/3 of the corpus generator (bench workloads `long`, `long1g`):
+    printable ASCII and '\\n' only; kind 2's lines average megabytes (a page
+    of short log lines now and then); kind 3's first 1 GiB holds no '\\n'
+    (checked on its first 64 MiB here)."""
+    import numpy as np
+
+    d = np.frombuffer(dgrep.synth_corpus_host(64 << 20, 3, 2), np.uint8)
+    assert bool(((d == 10) | ((d >= 0x20) & (d < 0x7f))).all())
+    nl = np.flatnonzero(d == 10)
+    gaps = np.diff(nl)
+    assert gaps.max() > (2 << 20)            # long lines
+    assert (gaps < 300).sum() > 100          # and pages of log lines
+    d3 = np.frombuffer(dgrep.synth_corpus_host(64 << 20, 3, 3), np.uint8)
+    assert not (d3 == 10).any()

@@ -127,7 +127,7 @@ def test_encode_device_capacity_retry(ctx):
     cap = 1 << 20
     ln = torch.empty(cap, dtype=torch.int64, device="cuda")
     st = torch.empty(cap, dtype=torch.int64, device="cuda")
-    le = torch.empty(cap, dtype=torch.int32, device="cuda")
+    le = torch.empty(cap, dtype=torch.int64, device="cuda")
     cnt = ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), cap)
     assert 0 < cnt <= cap
     small = torch.empty(1000, dtype=torch.uint8, device="cuda")

@@ -1,0 +1,134 @@
+"""Long lines on the GPU (application/grep.go:17 splits a file of any shape;
+map_reduce/worker.go:72-76 reads whole files). A lane whose chunk holds no
+'\\n' owns no line and stops at its chunk end; on the <= 256-state steppers a
+line still open two chunks past its owner's chunk is parked and finished by the
+long-line kernels (end from the per-chunk '\\n' counts, per-segment transition
+maps composed in order) -- checked bit-exactly against the oracle for every
+such stepper, with matches at a line's start, middle and far end, lines ending
+exactly at chunk edges, newline-free and unterminated splits. A line over
+4 GiB is reported with its 64-bit length (structural check: the oracle's
+32-bit lengths cannot hold it)."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(ctx, pattern, data, threads=16):
+    ctx.load(pattern)
+    ln, st, le = ctx.scan(data)
+    oln, ost, ole = O.grep_map(pattern, data, threads=threads)
+    assert len(ln) == len(oln), (pattern, len(ln), len(oln))
+    np.testing.assert_array_equal(ln, oln)
+    np.testing.assert_array_equal(st, ost)
+    np.testing.assert_array_equal(le.astype(np.uint64), ole.astype(np.uint64))
+    return ctx.scan_stats()
+
+
+def _long_split(seed, sizes, plant=b"error"):
+    rnd = random.Random(seed)
+    parts = []
+    for L in sizes:
+        body = bytearray(rnd.choice(b"abcdfghij ") for _ in range(L))
+        where = rnd.random()
+        if where < 0.25 and L > 10:
+            body[:5] = plant
+        elif where < 0.5 and L > 10:
+            body[-5:] = plant
+        elif where < 0.75 and L > 10:
+            q = rnd.randrange(L - 5)
+            body[q:q + 5] = plant
+        parts.append(bytes(body))
+    return b"\n".join(parts)
+
+
+STEPPER_PATTERNS = [
+    ("auto", b"error"),                                   # Sheng (<= 8 states)
+    ("auto", b""),                                        # every line
+    ("auto", b"^[a-j ]*error[a-j ]*$"),                   # pair stepper
+    ("table", b"error$"),                                 # u8 table, two chunks per lane
+    ("auto", b"(?i)e[r]+or"),
+]
+
+
+@pytest.mark.parametrize("force,pattern", STEPPER_PATTERNS)
+def test_long_lines_parked_and_resolved(gpu_ctx, force, pattern):
+    sizes = [10, 300, 70000, 5, 1 << 20, 3 << 20, 40000, 9000, 100, (1 << 22) + 7, 2]
+    data = _long_split(5, sizes)
+    try:
+        gpu_ctx.set_stepper(force)
+        st = _check(gpu_ctx, pattern, data)
+        assert st["pending"] > 0, st  # some lines were parked and resolved
+        # unterminated last line that is long, and a newline-free split
+        _check(gpu_ctx, pattern, data + b"\n" + b"x" * 200000 + b"error")
+        _check(gpu_ctx, pattern, b"y" * (3 << 20) + b"error" + b"z" * 100000)
+        _check(gpu_ctx, pattern, b"error" + b"y" * (3 << 20))
+    finally:
+        gpu_ctx.set_stepper("auto")
+
+
+@pytest.mark.parametrize("chunk", [4096, 8192, 32768])
+def test_long_lines_at_chunk_edges(gpu_ctx, chunk):
+    """Lines ending exactly at chunk boundaries and at 2 C (the parking point)."""
+    gpu_ctx.set_lane_chunk(chunk)
+    try:
+        for extra in (-1, 0, 1):
+            sizes = [chunk - 1, 2 * chunk + extra, 3 * chunk - 1, 5 * chunk + extra, chunk * 64 + extra, 7]
+            data = _long_split(11 + extra, sizes)
+            _check(gpu_ctx, b"error", data)
+            _check(gpu_ctx, b"", data)
+    finally:
+        gpu_ctx.set_lane_chunk(0)
+
+
+def test_long_lines_workload_scale(gpu_ctx):
+    """Hundreds of 64 KiB-8 MiB lines mixed with normal log lines."""
+    import dgrep
+
+    rnd = random.Random(21)
+    parts = []
+    for i in range(120):
+        if rnd.random() < 0.5:
+            parts.append(dgrep.synth_corpus_host(rnd.randrange(1, 200000), 100 + i, 0).rstrip(b"\n"))
+        else:
+            L = rnd.randrange(64 << 10, 8 << 20)
+            b = bytearray(b"q" * L)
+            if rnd.random() < 0.5:
+                q = rnd.randrange(L - 5)
+                b[q:q + 5] = b"error"
+            parts.append(bytes(b))
+    data = b"\n".join(parts)
+    st = _check(gpu_ctx, b"error", data)
+    assert st["pending"] > 10
+
+
+def test_line_over_4gib(gpu_ctx):
+    """One 4.5 GiB line (no '\\n') then a short one: the "" pattern (the
+    reference's shipped grep.go:11) matches both; `error` planted 3 bytes
+    before the long line's end matches only it. Checked structurally: record
+    = whole line, 64-bit length, numbering."""
+    import torch
+
+    n_long = (9 << 29) + 3  # 4.5 GiB + 3
+    tail = b"\nabc"
+    n = n_long + len(tail)
+    buf = torch.full((n + 64,), ord("x"), dtype=torch.uint8, device="cuda")
+    buf[n_long - 8:n_long - 3] = torch.tensor(list(b"error"), dtype=torch.uint8, device="cuda")
+    buf[n_long:n] = torch.tensor(list(tail), dtype=torch.uint8, device="cuda")
+    cap = 16
+    line_t = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    start_t = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    len_t = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    for pattern, want in ((b"", [(1, 0, n_long), (2, n_long + 1, 3)]), (b"error", [(1, 0, n_long)]),
+                          (b"^x*$", [])):
+        gpu_ctx.load(pattern)
+        cnt = gpu_ctx.scan_device(buf.data_ptr(), n, line_t.data_ptr(), start_t.data_ptr(), len_t.data_ptr(), cap)
+        got = list(zip(line_t[:cnt].tolist(), start_t[:cnt].tolist(), len_t[:cnt].tolist()))
+        assert got == want, (pattern, got)
+        assert gpu_ctx.scan_stats()["pending"] >= 1
+    del buf
+    torch.cuda.empty_cache()

@@ -55,15 +55,16 @@ def _check(ctx, pattern, data, threads=1):
     return len(ln)
 
 
-def test_synth_device_matches_host(gpu_ctx):
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_synth_device_matches_host(gpu_ctx, kind):
     import torch
     import dgrep
 
-    n = (1 << 20) + 12345
+    n = (1 << 22) + 12345
     buf = torch.empty(n, dtype=torch.uint8, device="cuda")
-    gpu_ctx.synth(buf.data_ptr(), n, 7, 1)
+    gpu_ctx.synth(buf.data_ptr(), n, 7, kind)
     torch.cuda.synchronize()
-    host = dgrep.synth_corpus_host(n, 7, 1)
+    host = dgrep.synth_corpus_host(n, 7, kind)
     assert buf.cpu().numpy().tobytes() == host
 
 
@@ -252,7 +253,7 @@ def test_adaptive_chunk_on_large_split_and_density_cap(gpu_ctx):
     cap = 40 << 20
     ln = torch.empty(cap, dtype=torch.int64, device="cuda")
     st = torch.empty(cap, dtype=torch.int64, device="cuda")
-    le = torch.empty(cap, dtype=torch.int32, device="cuda")
+    le = torch.empty(cap, dtype=torch.int64, device="cuda")
     chunks = {}
     for pattern in ("error", "r"):
         gpu_ctx.load(pattern)
@@ -290,14 +291,14 @@ def test_scan_device_resident(gpu_ctx):
     cap = 1 << 20
     ln = torch.empty(cap, dtype=torch.int64, device="cuda")
     st = torch.empty(cap, dtype=torch.int64, device="cuda")
-    le = torch.empty(cap, dtype=torch.int32, device="cuda")
+    le = torch.empty(cap, dtype=torch.int64, device="cuda")
     cnt = gpu_ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), cap)
     host = buf.cpu().numpy().tobytes()
     oln, ost, ole = O.grep_map(b"error", host, threads=16)
     assert cnt == len(oln)
     np.testing.assert_array_equal(ln[:cnt].cpu().numpy().astype(np.uint64), oln)
     np.testing.assert_array_equal(st[:cnt].cpu().numpy().astype(np.uint64), ost)
-    np.testing.assert_array_equal(le[:cnt].cpu().numpy().astype(np.uint32), ole)
+    np.testing.assert_array_equal(le[:cnt].cpu().numpy().astype(np.uint64), ole)
     # capacity too small: count reported, caller retries
     cnt2 = gpu_ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), 10)
     assert cnt2 == cnt

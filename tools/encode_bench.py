@@ -43,7 +43,7 @@ def main():
     cap = max(1 << 16, n // 2048)
     ln = torch.empty(cap, dtype=torch.int64, device="cuda")
     st = torch.empty(cap, dtype=torch.int64, device="cuda")
-    le = torch.empty(cap, dtype=torch.int32, device="cuda")
+    le = torch.empty(cap, dtype=torch.int64, device="cuda")
     cnt = ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), cap)
     assert cnt <= cap
     fname = "split-%s.log" % args.workload
