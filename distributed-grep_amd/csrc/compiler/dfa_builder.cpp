@@ -725,7 +725,7 @@ int build_dfa(const Re& re, CompiledDfa* out, std::string* err, size_t state_bud
   // over the DFA budget: the first states as a filter, the NFA program decides
   // the lines that leave them (DGREP_DFA_PARTIAL)
   if (part.nstates < 3 || !b.nfa_program(&part.nfa)) {
-    *err = "DFA exceeds the state budget and the NFA has more than 256 rune-set positions";
+    *err = "DFA exceeds the state budget and the NFA has more than 1024 rune-set positions";
     return DGREP_E_TOO_LARGE;
   }
   *out = std::move(part);

@@ -143,6 +143,7 @@ struct VerifyArgs {
   uint32_t matched;
   // resolved pending long lines (StagedLine kMetaPend: len_lo = index)
   const PendingLine* pend;
+  uint32_t nfa_words;  // the NFA program's position-set words (nw)
 };
 
 // LDS slot records (8 B: start16 | rel16, then w1): w1 = the line's length with

@@ -1282,11 +1282,14 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
 // ---- NFA verification (DGREP_DFA_PARTIAL) -----------------------------------
 // A pattern whose DFA exceeds the compiler's budget ships its first DFA states
 // (the filter) and an NFA program (include/dgrep_blob.h): per rune class, a
-// bit-parallel step over at most 256 positions (the NFA's rune-set states),
+// bit-parallel step over at most 1024 positions (the NFA's rune-set states),
 // with the UTF-8 decoder trie and the context flags (line start, previous rune
 // a word character) the DFA construction uses. One lane per candidate line;
-// the program is small and stays in L2.
+// the program is small and stays in L2. The position sets live in registers:
+// the kernel is instantiated for up to 256 positions (8 words, the common
+// case) and up to DGREP_NFA_MAX_POS (32 words).
 constexpr uint32_t kNfaMaxWords = DGREP_NFA_MAX_POS / 32;
+constexpr uint32_t kNfaSmallWords = 8;
 
 struct NfaView {
   const int32_t* child;
@@ -1324,25 +1327,27 @@ __device__ __forceinline__ NfaView nfa_view(const uint32_t* g) {
   return n;
 }
 
+template <uint32_t NW>
 struct NfaRun {
-  uint32_t P[kNfaMaxWords];  // positions consumed by the last rune
+  uint32_t P[NW];  // positions consumed by the last rune
   uint32_t begin, pw, node;  // no rune yet on the line; previous rune is a word char; decoder node
   bool matched;
 };
 
 // one rune of class c (DfaBuilder::step, per position)
-__device__ __forceinline__ void nfa_rune(const NfaView& g, NfaRun& r, uint32_t c) {
+template <uint32_t NW>
+__device__ __forceinline__ void nfa_rune(const NfaView& g, NfaRun<NW>& r, uint32_t c) {
   const uint32_t nwf = g.word[c];
   const uint32_t ctx = g.has_word ? r.pw * 2u + nwf : 0u;
   const uint32_t nw = g.nw;
   const uint32_t* ini = g.init + (size_t(r.begin) * g.nctx + ctx) * nw;
   const uint32_t* mx = g.mx + size_t(ctx) * nw;
   bool m = g.init_m[r.begin * g.nctx + ctx] != 0u;
-  uint32_t S[kNfaMaxWords];
+  uint32_t S[NW];
 #pragma unroll
-  for (uint32_t j = 0; j < kNfaMaxWords; ++j) S[j] = j < nw ? ini[j] : 0u;
+  for (uint32_t j = 0; j < NW; ++j) S[j] = j < nw ? ini[j] : 0u;
 #pragma unroll
-  for (uint32_t w = 0; w < kNfaMaxWords; ++w) {
+  for (uint32_t w = 0; w < NW; ++w) {
     uint32_t bits = r.P[w];
     if (bits & (w < nw ? mx[w] : 0u)) m = true;
     while (bits) {
@@ -1350,7 +1355,7 @@ __device__ __forceinline__ void nfa_rune(const NfaView& g, NfaRun& r, uint32_t c
       bits &= bits - 1u;
       const uint32_t* row = g.cl + (size_t(x) * g.nctx + ctx) * nw;
 #pragma unroll
-      for (uint32_t j = 0; j < kNfaMaxWords; ++j)
+      for (uint32_t j = 0; j < NW; ++j)
         if (j < nw) S[j] |= row[j];
     }
   }
@@ -1360,14 +1365,15 @@ __device__ __forceinline__ void nfa_rune(const NfaView& g, NfaRun& r, uint32_t c
   }
   const uint32_t* hc = g.has + size_t(c) * nw;
 #pragma unroll
-  for (uint32_t j = 0; j < kNfaMaxWords; ++j) r.P[j] = j < nw ? (S[j] & hc[j]) : 0u;
+  for (uint32_t j = 0; j < NW; ++j) r.P[j] = j < nw ? (S[j] & hc[j]) : 0u;
   r.begin = 0;
   r.pw = g.has_word ? nwf : 0u;
 }
 
 // one byte through the UTF-8 decoder trie (Go's utf8.DecodeRune: a byte that
 // breaks a sequence flushes its pending bytes as U+FFFD and is decoded afresh)
-__device__ __forceinline__ void nfa_byte(const NfaView& g, NfaRun& r, uint32_t b) {
+template <uint32_t NW>
+__device__ __forceinline__ void nfa_byte(const NfaView& g, NfaRun<NW>& r, uint32_t b) {
   int32_t v = g.child[size_t(r.node) * 256 + b];
   if (r.node != 0 && v == -1) {
     for (uint32_t i = 0, d = g.depth[r.node]; i < d && !r.matched; ++i) nfa_rune(g, r, g.fffd);
@@ -1385,10 +1391,11 @@ __device__ __forceinline__ void nfa_byte(const NfaView& g, NfaRun& r, uint32_t b
   }
 }
 
+template <uint32_t NW>
 __device__ __forceinline__ bool nfa_line_matches(const NfaView& g, const uint8_t* data, uint64_t a, uint64_t e) {
-  NfaRun r;
+  NfaRun<NW> r;
 #pragma unroll
-  for (uint32_t j = 0; j < kNfaMaxWords; ++j) r.P[j] = 0;
+  for (uint32_t j = 0; j < NW; ++j) r.P[j] = 0;
   r.begin = 1;
   r.pw = 0;
   r.node = 0;
@@ -1402,7 +1409,7 @@ __device__ __forceinline__ bool nfa_line_matches(const NfaView& g, const uint8_t
   bool m = g.end_init[r.begin * 2u + r.pw] != 0u;
   const uint32_t* ex = g.end_x + size_t(r.pw) * g.nw;
 #pragma unroll
-  for (uint32_t w = 0; w < kNfaMaxWords; ++w)
+  for (uint32_t w = 0; w < NW; ++w)
     if (w < g.nw && (r.P[w] & ex[w])) m = true;
   return m;
 }
@@ -1556,9 +1563,10 @@ __global__ __launch_bounds__(256) void long_fin_kernel(LongArgs la) {
   }
 }
 
+template <uint32_t NW>
 __global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
   const NfaView g = nfa_view(v.nfa);
-  verify_tiles(v, [&](uint64_t a, uint64_t e) { return nfa_line_matches(g, v.data, a, e); });
+  verify_tiles(v, [&](uint64_t a, uint64_t e) { return nfa_line_matches<NW>(g, v.data, a, e); });
 }
 
 // ---- ordering passes ------------------------------------------------------
@@ -1856,8 +1864,10 @@ hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t s
   if (grid == 0) return hipSuccess;
   if (!candidates)
     hipLaunchKernelGGL(resolve_tiles_kernel, dim3(grid), dim3(256), 0, stream, v);
+  else if (v.nfa && v.nfa_words <= kNfaSmallWords)
+    hipLaunchKernelGGL(verify_nfa_kernel<kNfaSmallWords>, dim3(grid), dim3(256), 0, stream, v);
   else if (v.nfa)
-    hipLaunchKernelGGL(verify_nfa_kernel, dim3(grid), dim3(256), 0, stream, v);
+    hipLaunchKernelGGL(verify_nfa_kernel<kNfaMaxWords>, dim3(grid), dim3(256), 0, stream, v);
   else if (v.full_u32)
     hipLaunchKernelGGL(verify_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, v);
   else

@@ -97,6 +97,7 @@ struct dgrep_ctx {
   uint32_t blob_matched = UINT32_MAX;          // the absorbing accepting state in d_full's ids (none: UINT32_MAX)
   uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
   uint32_t* d_nfa = nullptr;                   // DGREP_DFA_PARTIAL: the NFA program (verify_nfa_kernel)
+  uint32_t nfa_words = 0;                      // its position-set words
   int blocks_per_cu = 1;
 
   // per-scan scratch (grown on demand, reused)
@@ -512,6 +513,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
       c->err = "dgrep_load_dfa: malformed NFA program";
       return DGREP_E_INVALID;
     }
+    c->nfa_words = prog[2];
     HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_nfa), h.nfa_bytes));
     HIPCHK(hipMemcpy(c->d_nfa, prog, h.nfa_bytes, hipMemcpyHostToDevice));
   } else if (filter_ok) {
@@ -866,6 +868,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.staging_cap = c->staging_cap;
     v.removed = c->d_counters + 3;  // zeroed before the scan
     v.nfa = c->d_nfa;
+    v.nfa_words = c->nfa_words;
     v.matched = c->d_nfa ? UINT32_MAX : c->blob_matched;
     v.pend = c->d_pend;
     HIPCHK(hipEventRecord(c->ev4, c->stream));

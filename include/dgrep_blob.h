@@ -68,6 +68,6 @@ typedef struct {
  * U+FFFD runes) it matches if end_init[begin][prev_word] or P & end_x[prev_word].
  */
 #define DGREP_NFA_MAGIC 0x3141464eu /* "NFA1" */
-#define DGREP_NFA_MAX_POS 256u
+#define DGREP_NFA_MAX_POS 1024u
 
 #endif

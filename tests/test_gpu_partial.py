@@ -26,7 +26,9 @@ def _ab_lines(rnd, n):
     return b"\n".join(out)
 
 
-HUGE = [b"[ab]*a[ab]{21}", b"a.{20}$", b"(?i)\\bk.{19}s"]
+HUGE = [b"[ab]*a[ab]{21}", b"a.{20}$", b"(?i)\\bk.{19}s",
+        # more than 256 NFA positions: verify_nfa_kernel's 32-word instance
+        b"[ab]*a[ab]{300}", b"x\\pL{280}y"]
 
 
 @pytest.mark.parametrize("pattern", HUGE)
@@ -37,6 +39,8 @@ def test_budget_exceeding_patterns_on_gpu(gpu_ctx, pattern):
     assert cp.partial, cp.flags
     rnd = random.Random(len(pattern))
     data = _ab_lines(rnd, 40000) + b"\n" + dgrep.synth_corpus_host(1 << 20, 5, 0)
+    # lines long enough for the > 256-position patterns to match
+    data += b"\n" + b"ab" * 200 + b"\n" + b"b" * 299 + b"\nx" + b"q" * 280 + b"y\nx" + "é".encode() * 280 + b"y"
     n = _check(gpu_ctx, cp, data, threads=16)
     st = gpu_ctx.scan_stats()
     assert st["stepper"] == "filter", st
