@@ -55,6 +55,18 @@ struct PendingLine {
   uint64_t end;
   uint64_t len;
 };
+// Sheng stepper (<= 8 states): per lane chunk, the transition map of its bytes
+// up to and including its first '\n' (first = that byte's chunk-relative
+// offset), or of the whole chunk (first = kNoNewline). Map byte s (lo: states
+// 0-3, hi: 4-7) = the stepper state reached from state s. A parked long line
+// is finished by composing the maps of the chunks it crosses (long_sheng_kernel).
+struct ChunkMap {
+  uint32_t lo, hi;
+  uint32_t first;
+  uint32_t pad;
+};
+constexpr uint32_t kNoNewline = 0xffffffffu;
+
 // a segment of a parked line's remaining bytes (long_map_kernel)
 struct LongSeg {
   uint64_t begin, end;
@@ -100,6 +112,8 @@ struct ScanArgs {
   PendingLine* pend;
   uint64_t pend_cap;
   unsigned long long* pend_count;
+  // Sheng stepper: the chunk maps instead of chunk_nl (nullptr: none)
+  ChunkMap* chunk_map;
 };
 
 // the long-line kernels' arguments (long_end / long_map / long_fin)
@@ -119,6 +133,11 @@ struct LongArgs {
   uint64_t nseg;
   const uint64_t* seg_off;  // [npend + 1]: line i's segments
   uint8_t* segmap;          // [nseg][256]
+  // Sheng stepper (long_sheng_kernel): the scan's chunk maps, stepper state
+  // ids, start_m as a stepper id and V['\n'] (the 8 next states of '\n')
+  const ChunkMap* chunk_map;
+  uint32_t sheng_m;
+  uint32_t nl_lo, nl_hi;
 };
 
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids

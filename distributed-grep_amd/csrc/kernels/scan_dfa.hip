@@ -59,7 +59,7 @@
 #define DGREP_SHENG_CHUNK 4096
 #endif
 #ifndef DGREP_SHENG_SLOTS
-#define DGREP_SHENG_SLOTS 24
+#define DGREP_SHENG_SLOTS 23  // + the dummy slot + the chunk-map slot: 3 workgroups per CU (159,744 B of LDS)
 #endif
 #ifndef DGREP_SHENG_BLOCK
 #define DGREP_SHENG_BLOCK 128
@@ -144,10 +144,11 @@ __device__ __forceinline__ uint32_t hi_byte(uint32_t m) { return (31u - __clz(m)
 // different states that read the same input byte hit different banks.
 constexpr uint32_t kRow = 260;
 
-template <int TBL, int E, int NT>
+template <int TBL, int E, int NT, bool MAPS = false>
 struct ScanSmem {
   alignas(16) uint8_t tbl[TBL];  // first member: the table sits at LDS address 0
   uint32_t slots[NT * E * 2];
+  uint2 maps[MAPS ? NT : 1];     // Sheng: each lane's chunk map between map-mode blocks
 };
 
 // DFA of at most 256 states: u8 transition table, row s at LDS s*260.
@@ -466,6 +467,11 @@ struct Emitter {
   uint2* spill = nullptr;    // slot mode: this lane's HBM spill area (nullptr: none)
   uint32_t spill_cap = 0;    // its records
   uint64_t* tail = nullptr;  // slot mode: this lane's ScanArgs::tails entry
+  // Sheng chunk maps (nullptr: none): this lane's ChunkMap record, and its LDS
+  // copy of the map while the chunk has shown no '\n' (kept out of registers:
+  // only the map-mode blocks hold it)
+  uint4* cmap = nullptr;
+  uint2* mapsl = nullptr;
 
   // cand: a filter candidate (verified afterwards)
   __device__ __forceinline__ void operator()(LaneRun& r, uint64_t q, int64_t start, uint32_t rel,
@@ -576,9 +582,10 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit);
 
-template <int J, class Step, int E, bool DIRECT>
+template <int J, bool MAP, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x, const typename Step::Pre& pre,
-                                          uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
+                                          uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit,
+                                          uint32_t& mlo, uint32_t& mhi) {
   // StepTable: keep each word's work in place (hoisting the chain-independent
   // newline masks of a whole block costs ~100 VGPRs). StepSheng8 wants the
   // opposite: its state-independent LDS reads should run ahead of the chain.
@@ -586,6 +593,15 @@ __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x
   const uint32_t m = nl_mask(x);
   uint32_t s0, s1, s2, s3;
   st.apply(pre, s, s0, s1, s2, s3);
+  if constexpr (MAP) {
+    // Sheng chunk map: every state at once (two v_perm per byte), up to and
+    // including the chunk's first '\n', whose offset completes the record
+    if (!b.past && b.nl0 + b.nlrun == 0u) {
+      const uint32_t k = m ? uint32_t(__builtin_ctz(m)) >> 3 : 3u;
+      st.compose(pre, k, mlo, mhi);
+      if (m) *emit.cmap = make_uint4(mlo, mhi, uint32_t(b.pos) + 4u * J + k, 0u);
+    }
+  }
   word_events<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
   s = s3;
 }
@@ -744,7 +760,7 @@ __device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uin
   blk_finish(bb, sb, rb);
 }
 
-template <int BK, class Step, int E, bool DIRECT>
+template <int BK, bool MAP, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
@@ -760,18 +776,27 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
     w[4 * i + 2] = v[i].z;
     w[4 * i + 3] = v[i].w;
   }
+  uint32_t mlo = 0, mhi = 0;
+  if constexpr (MAP) {
+    const uint2 v = *emit.mapsl;
+    mlo = v.x;
+    mhi = v.y;
+  }
   typename Step::Pre pre = st.prep(w[0]);
 #define DG_W(J)                                                                         \
   if ((J) < NW) {                                                                       \
     const typename Step::Pre cur = pre;                                                 \
     if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : 0]);                     \
-    word_step<J>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit);                     \
+    word_step<J, MAP>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit, mlo, mhi);      \
   }
   DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
   DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
   DG_W(16) DG_W(17) DG_W(18) DG_W(19) DG_W(20) DG_W(21) DG_W(22) DG_W(23)
   DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
 #undef DG_W
+  if constexpr (MAP) {
+    if (b.nl0 + b.nlrun == 0u) *emit.mapsl = make_uint2(mlo, mhi);
+  }
   blk_finish(b, s, r);
 }
 
@@ -789,11 +814,29 @@ __device__ __forceinline__ void load_block(uint4 (&v)[BK / 16], const uint8_t* p
 template <class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8_t* p, uint64_t pos, uint64_t avail, uint64_t C,
                          LaneRun& r, uint32_t& nl_chunk, bool& snap, const Emitter<E, DIRECT>& emit) {
+  // Sheng chunk map: continued byte by byte while the chunk shows no '\n'
+  const bool tm = Step::kKind == kStepSheng8 && emit.cmap && r.nl == 0u && pos < C;
+  uint32_t mlo = 0, mhi = 0;
+  if (tm) {
+    const uint2 v = *emit.mapsl;
+    mlo = v.x;
+    mhi = v.y;
+  }
   for (; pos < avail; ++pos) {
-    if (pos == C) { nl_chunk = r.nl; snap = true; }
+    if (pos == C) {
+      nl_chunk = r.nl;
+      snap = true;
+      if (tm && r.nl == 0u) *emit.cmap = make_uint4(mlo, mhi, kNoNewline, 0u);
+    }
     if (pos >= C && (r.term || !r.seen)) return;
     const uint32_t b = p[pos];
     const uint32_t s1 = st.byte(r.s, b);
+    if constexpr (Step::kKind == kStepSheng8) {
+      if (tm && r.nl == 0u && pos < C) {
+        st.compose_byte(b, mlo, mhi);
+        if (b == '\n') *emit.cmap = make_uint4(mlo, mhi, uint32_t(pos), 0u);
+      }
+    }
 
     if (b == '\n') {
       if (Step::is(s1, M) && r.seen && !(pos >= C && r.term)) emit(r, pos, r.prev_nl + 1, r.nl, cand_of(st, s1));
@@ -804,6 +847,8 @@ __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8
     }
     r.s = s1;
   }
+  // the split ends inside the chunk (or at its end) before any '\n'
+  if (tm && r.nl == 0u && avail <= C) *emit.cmap = make_uint4(mlo, mhi, kNoNewline, 0u);
   const uint32_t se = st.byte(r.s, uint32_t('\n'));
   if (!r.term && r.seen && Step::is(se, M)) emit(r, avail, r.prev_nl + 1, r.nl, cand_of(st, se));
 }
@@ -841,19 +886,26 @@ __device__ __forceinline__ bool lane_done(uint64_t pos, uint64_t C, const LaneRu
   return pos >= C && (r.term || !r.seen);
 }
 
+// Sheng with chunk maps: a line still open kParkAfter bytes past the chunk end
+// is parked at the chunk end (its state there was kept in the lane's map slot);
+// the resolution composes the maps of the chunks from C on, so the owner's
+// extra work is bounded by kParkAfter instead of a whole chunk.
+constexpr uint64_t kParkAfter = 4096;
+static_assert(kParkAfter % Tune<StepSheng8>::B == 0, "park point must be a block boundary");
+
 // The lane's last line is still open at 2 C (it started in the lane's chunk and
 // crossed the whole next one): park it as PENDING -- state and position go to
 // the pending list, the lane's record for it is resolved by the long-line
 // kernels -- instead of reading on alone.
 template <class Step, int E>
 __device__ __forceinline__ void park_pending(const ScanArgs& a, uint64_t cs, uint64_t pos, LaneRun& r,
-                                             const Emitter<E, false>& emit) {
+                                             const Emitter<E, false>& emit, uint32_t s) {
   const unsigned long long idx = atomicAdd(a.pend_count, 1ull);
   if (idx < a.pend_cap) {
     PendingLine P;
     P.line_start = cs + uint64_t(r.prev_nl + 1);
     P.resume = cs + pos;
-    P.state = park_index<Step>(a, r.s);
+    P.state = park_index<Step>(a, s);
     P.matched = 0;
     P.len = 0;
     a.pend[idx] = P;
@@ -885,16 +937,39 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   uint4 A[BK / 16], B[BK / 16];
   constexpr bool kTrack = track_long<Step, DIRECT>();
   const bool park = kTrack && a.pend != nullptr;
+  // Sheng chunk maps (a.chunk_map): a block goes through the map-tracking copy
+  // while any lane of the wave has not met its chunk's first '\n' yet
+  // (wave-uniform branch; in text, the first few blocks of a chunk)
+  constexpr bool kMap = kTrack && Step::kKind == kStepSheng8;
+  const bool maps = kMap && emit.cmap != nullptr;
+  if (maps && pos0 == 0) *emit.mapsl = make_uint2(0x03020100u, 0x07060504u);  // identity
   if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
-  // a block inside the chunk goes through the map-tracking copy while any lane
-  // of the wave still looks for its chunk's first '\n' (wave-uniform branch)
-#define DG_STEP(V) run_block<BK>(st, M, V, pos, uint64_t(C), r, emit);
+#define DG_STEP(V)                                                                         \
+  if (kMap && __ballot(maps && r.nl == 0u && pos < uint64_t(C)) != 0)                      \
+    run_block<BK, kMap>(st, M, V, pos, uint64_t(C), r, emit);                              \
+  else                                                                                     \
+    run_block<BK, false>(st, M, V, pos, uint64_t(C), r, emit);
 #define DG_CHECK                                                                           \
-  if (pos == uint64_t(C)) { nl_chunk = r.nl; snap = true; }                                \
+  if (pos == uint64_t(C)) {                                                                \
+    nl_chunk = r.nl;                                                                       \
+    snap = true;                                                                           \
+    if (kMap && maps) {                                                                    \
+      if (r.nl == 0u) {                                                                    \
+        const uint2 mv = *emit.mapsl; /* the whole chunk: no '\n' in it */                \
+        *emit.cmap = make_uint4(mv.x, mv.y, kNoNewline, 0u);                               \
+      }                                                                                    \
+      emit.mapsl->x = r.s; /* the state at C: a line still open at C + kParkAfter */       \
+    }                                                                                      \
+  }                                                                                        \
   if (lane_done(pos, uint64_t(C), r)) break;                                               \
   if constexpr (kTrack) {                                                                  \
-    if (park && pos == 2 * uint64_t(C)) {                                                  \
-      park_pending<Step, E>(a, cs, pos, r, emit);                                          \
+    if (maps && pos == uint64_t(C) + kParkAfter) {                                         \
+      /* parked at C: the chunk maps from C on finish it */                                \
+      park_pending<Step, E>(a, cs, uint64_t(C), r, emit, emit.mapsl->x);                   \
+      break;                                                                               \
+    }                                                                                      \
+    if (park && !maps && pos == 2 * uint64_t(C)) {                                         \
+      park_pending<Step, E>(a, cs, pos, r, emit, r.s);                                     \
       break;                                                                               \
     }                                                                                      \
   }                                                                                        \
@@ -1006,7 +1081,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   // per-lane slot stride: E slots per stream, plus the dummy of flat_emit
   constexpr int ES = E * streams_of<Step, TBL>() + (flat_emit<Step, false>() ? 1 : 0);
   static_assert(!flat_emit<Step, false>() || streams_of<Step, TBL>() == 1, "dummy slot: one stream per lane");
-  __shared__ ScanSmem<TBL, ES, NT> sm;
+  __shared__ ScanSmem<TBL, ES, NT, Step::kKind == kStepSheng8> sm;
   const int tid = int(threadIdx.x);
   for (uint32_t i = uint32_t(tid) * 16u; i < a.table_bytes; i += NT * 16u)
     *reinterpret_cast<uint4*>(sm.tbl + i) = *reinterpret_cast<const uint4*>(a.table + i);
@@ -1039,6 +1114,12 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
     } else {
       Emitter<E, false> em{&a, slots, cs[0], 0, 0};
       em.tail = tails;
+      if constexpr (Step::kKind == kStepSheng8) {
+        if (a.chunk_map && cs[0] < a.n) {
+          em.cmap = reinterpret_cast<uint4*>(a.chunk_map + t * kTileLanes + uint64_t(lane));
+          em.mapsl = &sm.maps[tid];
+        }
+      }
       if (a.spill) {
         em.spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane;
         em.spill_cap = a.spill_per_lane;
@@ -1053,6 +1134,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         for (int k = 0; k < S; ++k)
           if (cs[k] < a.n) a.chunk_nl[t * kTileLanes * S + uint64_t(k) * kTileLanes + uint64_t(lane)] = nlc[k];
       }
+
     }
 
     // tile-wide exclusive scans of (newlines, matching lines) over the tile's
@@ -1563,6 +1645,102 @@ __global__ __launch_bounds__(256) void long_fin_kernel(LongArgs la) {
   }
 }
 
+// Sheng stepper (<= 8 states): the scan left every lane chunk's map
+// (ChunkMap), so a parked line is finished without reading its bytes again:
+// from its parked state, apply the whole-chunk maps of the chunks after the
+// park position, in order, up to the first chunk holding a '\n', whose map
+// ends with that '\n' (the line matches iff the state is then start_m); or,
+// no '\n' to the split's end, the last chunk's map and then V['\n'] (the
+// split's unterminated last line, grep.go:17). One workgroup per parked line:
+// each thread composes kLsPer consecutive chunk maps, the wave and then the
+// workgroup compose theirs in order (v_perm on 8-state byte maps).
+constexpr int kLsThreads = 256;
+constexpr int kLsPer = 4;
+
+// the map "a, then b" (byte s = b[a[s]])
+__device__ __forceinline__ uint2 map_then(uint2 a, uint2 b) {
+  return make_uint2(__builtin_amdgcn_perm(b.y, b.x, a.x), __builtin_amdgcn_perm(b.y, b.x, a.y));
+}
+
+__global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
+  __shared__ uint2 wmap[kLsThreads / 64];
+  __shared__ uint32_t whit[kLsThreads / 64];
+  __shared__ uint64_t wend[kLsThreads / 64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint2 ident = make_uint2(0x03020100u, 0x07060504u);
+  for (uint64_t i = blockIdx.x; i < la.npend; i += gridDim.x) {
+    const PendingLine P = la.pend[i];
+    uint32_t s = P.state;
+    uint64_t end = la.n;
+    for (uint64_t c0 = P.resume / la.chunk;; c0 += uint64_t(kLsThreads) * kLsPer) {
+      // this thread's chunks, in order, up to the first that holds a '\n' (or
+      // lies past the split)
+      const uint64_t cb = c0 + uint64_t(threadIdx.x) * kLsPer;
+      ChunkMap cm[kLsPer];
+#pragma unroll
+      for (int j = 0; j < kLsPer; ++j) {
+        const uint4 v = cb + j < la.nchunks ? *reinterpret_cast<const uint4*>(la.chunk_map + cb + j)
+                                            : make_uint4(0u, 0u, kNoNewline, 1u);  // pad 1: past the split
+        cm[j] = ChunkMap{v.x, v.y, v.z, v.w};
+      }
+      uint2 m = ident;
+      bool stop = false;
+      uint64_t e = 0;
+#pragma unroll
+      for (int j = 0; j < kLsPer; ++j) {
+        if (stop) continue;
+        if (cm[j].pad) {  // past the split's end
+          stop = true;
+          e = la.n;
+        } else {
+          m = map_then(m, make_uint2(cm[j].lo, cm[j].hi));
+          if (cm[j].first != kNoNewline) {
+            stop = true;
+            e = (cb + j) * la.chunk + cm[j].first;
+          }
+        }
+      }
+      // the wave: threads up to its first stopping one, composed in order
+      const uint64_t hb = __ballot(stop);
+      const uint32_t hl = hb ? uint32_t(__builtin_ctzll(hb)) : 64u;
+      if (lane > hl) m = ident;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint2 o = make_uint2(__shfl_down(m.x, d, 64), __shfl_down(m.y, d, 64));
+        if ((lane & uint32_t(2 * d - 1)) == 0u && lane + uint32_t(d) < 64u) m = map_then(m, o);
+      }
+      if (lane == 0) {
+        wmap[w] = m;
+        whit[w] = hl;
+      }
+      if (lane == hl) wend[w] = e;
+      __syncthreads();
+      uint32_t wf = kLsThreads / 64;
+      for (uint32_t k = 0; k < kLsThreads / 64; ++k) {
+        if (wf == kLsThreads / 64) {
+          const uint2 t = wmap[k];
+          s = __builtin_amdgcn_perm(t.y, t.x, s) & 0xffu;
+          if (whit[k] < 64u) wf = k;
+        }
+      }
+      if (wf < kLsThreads / 64) end = wend[wf];
+      __syncthreads();  // wmap / whit / wend are rewritten by the next round
+      if (wf < kLsThreads / 64) break;
+    }
+    // end < n: the last map ended with the line's '\n'; end == n: the split
+    // ended first, and its end closes the line (V['\n'] applied)
+    if (end == la.n) s = __builtin_amdgcn_perm(la.nl_hi, la.nl_lo, s) & 0xffu;
+    if (threadIdx.x == 0) {
+      PendingLine Q = P;
+      Q.end = end;
+      Q.len = end - P.line_start;
+      Q.matched = s == la.sheng_m ? 1u : 0u;
+      la.pend[i] = Q;
+    }
+    __syncthreads();
+  }
+}
+
 template <uint32_t NW>
 __global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
   const NfaView g = nfa_view(v.nfa);
@@ -1574,82 +1752,61 @@ __global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
 // compute, per tile, its first output index (exclusive scan of counts) and the
 // 1-based number of its first line (1 + exclusive scan of newline counts), then
 // copy every tile's lines to their final place in split order.
-constexpr int kOrdThreads = 256;
-constexpr int kOrdPerThread = 16;
-constexpr int kOrdTiles = kOrdThreads * kOrdPerThread;  // tiles per ordering block
+// The scan of the per-tile counts is ONE workgroup (a 16 GiB split at 32 KiB
+// chunks is 8,192 tiles = 128 KiB of TileInfo: 8 per thread, one pass), so the
+// ordering is two launches: tile_scan_kernel, order_lines_kernel.
+constexpr int kTsThreads = 1024;
+constexpr int kTsPer = 8;
 
-__device__ __forceinline__ void block_excl_scan2(uint64_t& a, uint64_t& b, uint64_t* sh_a, uint64_t* sh_b,
-                                                 uint64_t& tot_a, uint64_t& tot_b) {
-  const int t = int(threadIdx.x);
-  sh_a[t] = a;
-  sh_b[t] = b;
-  __syncthreads();
-  for (int d = 1; d < kOrdThreads; d <<= 1) {
-    uint64_t xa = 0, xb = 0;
-    if (t >= d) { xa = sh_a[t - d]; xb = sh_b[t - d]; }
+__global__ __launch_bounds__(kTsThreads) void tile_scan_kernel(const TileInfo* tiles, uint64_t ntiles,
+                                                               uint64_t* out_off, uint64_t* line_base) {
+  __shared__ unsigned long long wc[kTsThreads / 64], wl[kTsThreads / 64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  unsigned long long carry_c = 0, carry_l = 0;
+  for (uint64_t t0 = 0; t0 < ntiles; t0 += uint64_t(kTsThreads) * kTsPer) {
+    const uint64_t b = t0 + uint64_t(threadIdx.x) * kTsPer;
+    uint32_t c[kTsPer], l[kTsPer];
+    unsigned long long sc = 0, sl = 0;
+#pragma unroll
+    for (int i = 0; i < kTsPer; ++i) {
+      c[i] = 0;
+      l[i] = 0;
+      if (b + i < ntiles) {
+        const TileInfo ti = tiles[b + i];
+        c[i] = ti.count;
+        l[i] = ti.nl;
+      }
+      sc += c[i];
+      sl += l[i];
+    }
+    unsigned long long ic = sc, il = sl;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long xc = __shfl_up(ic, d, 64), xl = __shfl_up(il, d, 64);
+      if (lane >= uint32_t(d)) { ic += xc; il += xl; }
+    }
+    if (lane == 63) { wc[w] = ic; wl[w] = il; }
     __syncthreads();
-    sh_a[t] += xa;
-    sh_b[t] += xb;
-    __syncthreads();
-  }
-  tot_a = sh_a[kOrdThreads - 1];
-  tot_b = sh_b[kOrdThreads - 1];
-  a = sh_a[t] - a;
-  b = sh_b[t] - b;
-  __syncthreads();
-}
-
-// pass 1: per ordering block, the sums of its tiles' counts and newlines
-__global__ __launch_bounds__(kOrdThreads) void tile_reduce_kernel(const TileInfo* tiles, uint64_t ntiles,
-                                                                   uint64_t* blk_cnt, uint64_t* blk_nl) {
-  __shared__ uint64_t sa[kOrdThreads], sb[kOrdThreads];
-  const uint64_t t0 = uint64_t(blockIdx.x) * kOrdTiles + uint64_t(threadIdx.x) * kOrdPerThread;
-  uint64_t c = 0, l = 0;
-  for (int i = 0; i < kOrdPerThread; ++i)
-    if (t0 + i < ntiles) { c += tiles[t0 + i].count; l += tiles[t0 + i].nl; }
-  uint64_t tc, tl;
-  block_excl_scan2(c, l, sa, sb, tc, tl);
-  if (threadIdx.x == 0) { blk_cnt[blockIdx.x] = tc; blk_nl[blockIdx.x] = tl; }
-}
-
-// pass 2: exclusive scan over the ordering blocks (one workgroup, any count)
-__global__ __launch_bounds__(kOrdThreads) void block_scan_kernel(uint64_t* blk_cnt, uint64_t* blk_nl, uint64_t nblk) {
-  __shared__ uint64_t sa[kOrdThreads], sb[kOrdThreads];
-  uint64_t carry_c = 0, carry_l = 0;
-  for (uint64_t b0 = 0; b0 < nblk; b0 += kOrdThreads) {
-    const uint64_t i = b0 + threadIdx.x;
-    uint64_t c = i < nblk ? blk_cnt[i] : 0, l = i < nblk ? blk_nl[i] : 0;
-    uint64_t tc, tl;
-    block_excl_scan2(c, l, sa, sb, tc, tl);
-    if (i < nblk) { blk_cnt[i] = carry_c + c; blk_nl[i] = carry_l + l; }
-    carry_c += tc;
-    carry_l += tl;
+    unsigned long long pc = carry_c + ic - sc, pl = carry_l + il - sl;
+    for (uint32_t j = 0; j < kTsThreads / 64; ++j) {
+      if (j < w) { pc += wc[j]; pl += wl[j]; }
+      carry_c += wc[j];
+      carry_l += wl[j];
+    }
+    __syncthreads();  // wc / wl are rewritten by the next round
+#pragma unroll
+    for (int i = 0; i < kTsPer; ++i) {
+      if (b + i < ntiles) {
+        out_off[b + i] = pc;
+        line_base[b + i] = pl + 1;
+      }
+      pc += c[i];
+      pl += l[i];
+    }
   }
 }
 
-// pass 3: per tile, its output offset and first line number
-__global__ __launch_bounds__(kOrdThreads) void tile_offsets_kernel(const TileInfo* tiles, uint64_t ntiles,
-                                                                    const uint64_t* blk_cnt, const uint64_t* blk_nl,
-                                                                    uint64_t* out_off, uint64_t* line_base) {
-  __shared__ uint64_t sa[kOrdThreads], sb[kOrdThreads];
-  const uint64_t t0 = uint64_t(blockIdx.x) * kOrdTiles + uint64_t(threadIdx.x) * kOrdPerThread;
-  uint64_t c = 0, l = 0;
-  for (int i = 0; i < kOrdPerThread; ++i)
-    if (t0 + i < ntiles) { c += tiles[t0 + i].count; l += tiles[t0 + i].nl; }
-  uint64_t tc, tl;
-  block_excl_scan2(c, l, sa, sb, tc, tl);
-  c += blk_cnt[blockIdx.x];
-  l += blk_nl[blockIdx.x];
-  for (int i = 0; i < kOrdPerThread; ++i) {
-    if (t0 + i >= ntiles) break;
-    out_off[t0 + i] = c;
-    line_base[t0 + i] = l + 1;
-    c += tiles[t0 + i].count;
-    l += tiles[t0 + i].nl;
-  }
-}
-
-// pass 4: one wave per tile copies its staged lines to their final slots (SoA)
+// one wave per tile copies its staged lines to their final slots (SoA)
 __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles, const StagedLine* staging,
                                                           uint64_t ntiles, const uint64_t* out_off,
                                                           const uint64_t* line_base, uint64_t staging_cap,
@@ -1817,19 +1974,11 @@ hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStr
   return dispatch(kind, a.table_bytes, OverflowOp{&a, nover, stream});
 }
 
-uint64_t order_blocks(uint64_t ntiles) { return (ntiles + kOrdTiles - 1) / kOrdTiles; }
-
-// out_off / line_base: ntiles entries; blk: 2 * order_blocks(ntiles) scratch
+// out_off / line_base: ntiles entries each
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
-                       uint64_t* line_base, uint64_t* blk, uint64_t staging_cap, uint64_t capacity,
-                       uint64_t* line_no, uint64_t* start, uint64_t* len, hipStream_t stream) {
-  const uint64_t nblk = order_blocks(ntiles);
-  uint64_t* blk_cnt = blk;
-  uint64_t* blk_nl = blk + nblk;
-  hipLaunchKernelGGL(tile_reduce_kernel, dim3(nblk), dim3(kOrdThreads), 0, stream, tiles, ntiles, blk_cnt, blk_nl);
-  hipLaunchKernelGGL(block_scan_kernel, dim3(1), dim3(kOrdThreads), 0, stream, blk_cnt, blk_nl, nblk);
-  hipLaunchKernelGGL(tile_offsets_kernel, dim3(nblk), dim3(kOrdThreads), 0, stream, tiles, ntiles, blk_cnt, blk_nl,
-                     out_off, line_base);
+                       uint64_t* line_base, uint64_t staging_cap, uint64_t capacity, uint64_t* line_no,
+                       uint64_t* start, uint64_t* len, hipStream_t stream) {
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kTsThreads), 0, stream, tiles, ntiles, out_off, line_base);
   uint64_t grid = (ntiles + 3) / 4;
   if (grid > 16384) grid = 16384;
   hipLaunchKernelGGL(order_lines_kernel, dim3(grid), dim3(256), 0, stream, tiles, staging, ntiles, out_off,
@@ -1855,6 +2004,12 @@ hipError_t long_lines_resolve(const LongArgs& la, hipStream_t stream) {
   uint64_t grid = (la.npend + 255) / 256;
   if (grid > 4096) grid = 4096;
   if (grid) hipLaunchKernelGGL(long_fin_kernel, dim3(grid), dim3(256), 0, stream, la);
+  return hipGetLastError();
+}
+
+hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream) {
+  const uint64_t grid = la.npend < 4096 ? la.npend : 4096;
+  if (grid) hipLaunchKernelGGL(long_sheng_kernel, dim3(grid), dim3(kLsThreads), 0, stream, la);
   return hipGetLastError();
 }
 

@@ -49,13 +49,13 @@ uint32_t scan_table_row();
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu);
 hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
 hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStream_t stream);
-uint64_t order_blocks(uint64_t ntiles);
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
-                       uint64_t* line_base, uint64_t* blk, uint64_t staging_cap, uint64_t capacity,
-                       uint64_t* line_no, uint64_t* start, uint64_t* len, hipStream_t stream);
+                       uint64_t* line_base, uint64_t staging_cap, uint64_t capacity, uint64_t* line_no,
+                       uint64_t* start, uint64_t* len, hipStream_t stream);
 hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t stream);
 hipError_t long_lines_end(const LongArgs& la, hipStream_t stream);
 hipError_t long_lines_resolve(const LongArgs& la, hipStream_t stream);
+hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream);
 uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
@@ -104,8 +104,7 @@ struct dgrep_ctx {
   TileInfo* d_tiles = nullptr;
   uint64_t* d_out_off = nullptr;
   uint64_t* d_line_base = nullptr;
-  uint64_t* d_blk = nullptr;
-  uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0, blk_cap = 0;
+  uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0;
   StagedLine* d_staging = nullptr;
   uint64_t staging_cap = 0;
   // device counters: [0] staging append counter, [1] overflow lanes, [2] status bits
@@ -118,6 +117,9 @@ struct dgrep_ctx {
   uint64_t tails_cap = 0;
   uint32_t* d_chunk_nl = nullptr;  // '\n' per chunk (ScanArgs::chunk_nl)
   uint64_t chunk_nl_cap = 0;
+  ChunkMap* d_chunk_map = nullptr;  // Sheng: per-chunk maps (ScanArgs::chunk_map)
+  uint64_t chunk_map_cap = 0;
+  uint32_t sheng_nl_lo = 0, sheng_nl_hi = 0;  // Sheng: V['\n']
   PendingLine* d_pend = nullptr;   // parked long lines
   uint64_t pend_cap = 0;
   // long lines: the blob's u8 [S][256] table and stepper state -> blob state
@@ -392,8 +394,8 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl,
-                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_tiles, c->d_out_off, c->d_line_base, c->d_blk, c->d_staging, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
+                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -604,6 +606,12 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
       for (uint32_t s = 0; s < S; ++s)
         t[size_t(b) * 8 + id[s]] = uint8_t(id[trans[size_t(s) * h.nclasses + h.byte_class[b]]]);
     start = id[h.start] * 0x01010101u;
+    // V['\n'] for the long-line kernel (a line the split's end closes)
+    c->sheng_nl_lo = c->sheng_nl_hi = 0;
+    for (int k = 0; k < 4; ++k) {
+      c->sheng_nl_lo |= uint32_t(t[size_t('\n') * 8 + k]) << (8 * k);
+      c->sheng_nl_hi |= uint32_t(t[size_t('\n') * 8 + 4 + k]) << (8 * k);
+    }
     start_m = top;
     st2id.assign(S, 0);
     for (uint32_t x = 0; x < S; ++x) st2id[id[x]] = x;
@@ -749,7 +757,6 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   if ((rc = grow(c, &c->d_tiles, &c->tiles_cap, ntiles)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_out_off, &c->off_cap, ntiles + 1)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_line_base, &c->lb_cap, ntiles + 1)) != DGREP_OK) return rc;
-  if ((rc = grow(c, &c->d_blk, &c->blk_cap, 2 * order_blocks(ntiles) + 2)) != DGREP_OK) return rc;
   // kStepFilter stages its candidates too: the staging buffer holds at least
   // the previous scan's staged lines, and grows (one re-scan) if they overflow
   const bool filt = c->step_kind == kStepFilter && c->cand_end != UINT32_MAX;
@@ -769,8 +776,14 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   if ((rc = grow(c, &c->d_tails, &c->tails_cap, uint64_t(grid) * threads * streams)) != DGREP_OK) return rc;
   const bool park = c->d_long_tbl != nullptr;
   const uint64_t nchunks = (n + chunk - 1) / chunk;
+  // Sheng: the chunk maps replace the '\n' counts (long_sheng_kernel)
+  const bool park_maps = park && c->step_kind == kStepSheng8;
   if (park) {
-    if ((rc = grow(c, &c->d_chunk_nl, &c->chunk_nl_cap, nchunks)) != DGREP_OK) return rc;
+    if (park_maps) {
+      if ((rc = grow(c, &c->d_chunk_map, &c->chunk_map_cap, nchunks)) != DGREP_OK) return rc;
+    } else if ((rc = grow(c, &c->d_chunk_nl, &c->chunk_nl_cap, nchunks)) != DGREP_OK) {
+      return rc;
+    }
     if (!c->d_pend && (rc = grow(c, &c->d_pend, &c->pend_cap, 1024)) != DGREP_OK) return rc;
   }
 
@@ -789,7 +802,8 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.overflow_count = c->d_counters + 1;
   a.pend_count = c->d_counters + 2;
   a.tails = c->d_tails;
-  a.chunk_nl = park ? c->d_chunk_nl : nullptr;
+  a.chunk_nl = park && !park_maps ? c->d_chunk_nl : nullptr;
+  a.chunk_map = park_maps ? c->d_chunk_map : nullptr;
   a.wide = c->d_wide;
   a.nclasses = c->nclasses;
   a.hot_entries = c->hot_entries;
@@ -808,6 +822,13 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   S.lane_chunk = chunk;
   S.lane_slots = slots;
   S.tiles = ntiles;
+  // The common case -- no overflowing lane, no parked line, no filter
+  // candidates -- takes ONE host synchronisation per scan: the ordering passes
+  // are queued right behind the scan (they read the tiles' counts on the device
+  // and never write past `capacity`) and the counters are read back after them.
+  // Anything else shows in the counters, and the ordering is queued again once
+  // the extra passes have run.
+  const bool speculate = !filt && capacity != 0;
   for (int attempt = 0; attempt < 3; ++attempt) {
     a.staging = c->d_staging;
     a.capacity = c->staging_cap;
@@ -819,6 +840,9 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     HIPCHK(scan_dfa(c->step_kind, a, grid, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
+    if (speculate)
+      HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
+                         d_line, d_start, d_len, c->stream));
     HIPCHK(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     float ms = 0.f;
@@ -872,7 +896,22 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.matched = c->d_nfa ? UINT32_MAX : c->blob_matched;
     v.pend = c->d_pend;
     HIPCHK(hipEventRecord(c->ev4, c->stream));
-    if (npend && (rc = resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) return rc;
+    if (npend && park_maps) {
+      LongArgs la;
+      memset(&la, 0, sizeof la);
+      la.n = n;
+      la.chunk = chunk;
+      la.nchunks = nchunks;
+      la.pend = c->d_pend;
+      la.npend = npend;
+      la.chunk_map = c->d_chunk_map;
+      la.sheng_m = c->start_m;
+      la.nl_lo = c->sheng_nl_lo;
+      la.nl_hi = c->sheng_nl_hi;
+      HIPCHK(long_lines_sheng(la, c->stream));
+    } else if (npend && (rc = resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) {
+      return rc;
+    }
     HIPCHK(verify_candidates(v, filt, c->stream));
     HIPCHK(hipEventRecord(c->ev5, c->stream));
     unsigned long long removed = 0;
@@ -886,10 +925,13 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   if (filt) c->staged_hint = staged;
   S.matches = total;
   *count = total;
-  if (total != 0 && total <= capacity)
-    HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->d_blk, c->staging_cap,
-                       capacity, d_line, d_start, d_len, c->stream));
-  if (over || (total != 0 && total <= capacity)) HIPCHK(hipStreamSynchronize(c->stream));
+  // the speculative ordering stands unless the overflow pass, the long-line
+  // resolution or the verification changed the staged lines since
+  const bool order = total != 0 && total <= capacity && (!speculate || over || npend);
+  if (order)
+    HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
+                       d_line, d_start, d_len, c->stream));
+  if (over || order) HIPCHK(hipStreamSynchronize(c->stream));
   if (over) {
     HIPCHK(hipEventElapsedTime(&S.overflow_ms, c->ev2, c->ev3));
     c->last_ms += S.overflow_ms;
