@@ -531,7 +531,7 @@ struct Emitter {
     const uint32_t w0 = start | (rel << 16);
     const uint32_t i = min(r.nev, uint32_t(E));
     *reinterpret_cast<uint2*>(slots + 2u * i) = make_uint2(w0, lw);
-    if (r.nev >= uint32_t(E) && r.nev - uint32_t(E) < spill_cap) spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
+    if (r.nev - uint32_t(E) < spill_cap) spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);  // wraps below E
     r.nev += own ? 1u : 0u;
   }
   __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
@@ -564,9 +564,22 @@ struct Blk {
   bool past;        // block lies at or beyond the chunk end
   uint32_t nl0;     // r.nl at block start
   uint32_t nlrun;   // '\n' in the words processed so far
-  uint32_t lastm;   // newline mask of the last word with a '\n' (0: none yet)
-  int lastj;        // its index
+  uint32_t lnl;     // last '\n' of the words processed so far, 8 * (block offset + 3); 0: none yet
 };
+// Block-relative position of the last '\n', kept as ONE register per block:
+// for word J with newline mask m, f = sat(K_J - ffbh(m)) with K_J = 32 J + 48
+// is 8 * (4 J + k + 3) for its last '\n' at byte k (ffbh = 24 - 8 k) and 0 for a
+// word without one (ffbh(0) = ~0u saturates), so lnl = max(lnl, f): three VALU
+// per word (as the mask + word index pair took), and the matching-line path
+// reads the line start with one shift instead of rebuilding it from the pair.
+template <int J>
+__device__ __forceinline__ uint32_t lnl_update(uint32_t lnl, uint32_t m) {
+  uint32_t t;
+  asm("v_ffbh_u32 %0, %1" : "=v"(t) : "v"(m));
+  return max(lnl, __builtin_elementwise_sub_sat(uint32_t(32 * J + 48), t));
+}
+// block offset of the '\n' that lnl (!= 0) records
+__device__ __forceinline__ uint32_t lnl_pos(uint32_t lnl) { return (lnl >> 3) - 3u; }
 
 // the steppers whose lanes carry the dummy slot (slot_stride): one stream per lane
 template <class Step, bool DIRECT>
@@ -652,20 +665,20 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
   if (!b.past && (m & (m - 1u)) == 0u) {
     // branch-free operands (selects, no nested exec-mask regions)
     const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
-    const uint32_t lastpos = uint32_t(b.pos) + 4u * uint32_t(b.lastj) + hi_byte(b.lastm | 1u);
-    const uint32_t prev = b.lastm ? lastpos : uint32_t(r.prev_nl);
+    // the line starts after the block's last '\n' so far, else after r.prev_nl
+    const uint32_t start = b.lnl ? uint32_t(b.pos) + (b.lnl >> 3) - 2u : uint32_t(r.prev_nl) + 1u;
     const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
     if constexpr (flat_emit<Step, DIRECT>())
-      emit.inner_flat(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk),
-                      r.seen | (b.lastm != 0));
-    else if (r.seen | (b.lastm != 0))
-      emit.inner(r, uint32_t(b.pos) + 4u * J + k, prev + 1u, b.nl0 + b.nlrun, cand_of(st, sk));
+      emit.inner_flat(r, uint32_t(b.pos) + 4u * J + k, start, b.nl0 + b.nlrun, cand_of(st, sk),
+                      r.seen | (b.lnl != 0));
+    else if (r.seen | (b.lnl != 0))
+      emit.inner(r, uint32_t(b.pos) + 4u * J + k, start, b.nl0 + b.nlrun, cand_of(st, sk));
     return;
   }
   const uint64_t q0 = b.pos + 4u * J;
-  const bool seen_w = r.seen || b.lastm != 0;
-  const bool term_w = r.term || (b.past && b.lastm != 0);
-  const int64_t prev_w = b.lastm ? int64_t(b.pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm)) : r.prev_nl;
+  const bool seen_w = r.seen || b.lnl != 0;
+  const bool term_w = r.term || (b.past && b.lnl != 0);
+  const int64_t prev_w = b.lnl ? int64_t(b.pos + lnl_pos(b.lnl)) : r.prev_nl;
   uint32_t evm;
   if constexpr (Step::kKind == kStepPair)
     evm = st.evm(s1, s3);
@@ -689,7 +702,7 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
 template <int J>
 __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
   b.nlrun = add_popc(b.nlrun, m);
-  if (m) { b.lastm = m; b.lastj = J; }
+  b.lnl = lnl_update<J>(b.lnl, m);
 }
 
 template <int J, class Step, int E, bool DIRECT>
@@ -705,16 +718,15 @@ __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const
   b.past = pos >= C;
   b.nl0 = r.nl;
   b.nlrun = 0;
-  b.lastm = 0;
-  b.lastj = -1;
+  b.lnl = 0;
 }
 
 __device__ __forceinline__ void blk_finish(const Blk& b, uint32_t s, LaneRun& r) {
   r.s = s;
   r.nl = b.nl0 + b.nlrun;
-  if (b.lastm) {
+  if (b.lnl) {
     r.seen = true;
-    r.prev_nl = int64_t(b.pos + 4u * uint32_t(b.lastj) + hi_byte(b.lastm));
+    r.prev_nl = int64_t(b.pos + lnl_pos(b.lnl));
     if (b.past) r.term = true;
   }
 }
