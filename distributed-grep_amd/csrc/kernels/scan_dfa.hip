@@ -104,6 +104,14 @@
 #define DGREP_PAIR_WAVES 3
 #endif
 // Filter (C4, > 256 states): one 1024-thread workgroup per CU shares one LDS image
+// pair / filter: the word's first chain read before the next word's class reads
+#ifndef DGREP_CHAIN_FIRST
+#define DGREP_CHAIN_FIRST 0
+#endif
+// word_events: skip the matching-line region with a wave-uniform branch
+#ifndef DGREP_EV_BALLOT
+#define DGREP_EV_BALLOT 0
+#endif
 #ifndef DGREP_FILTER_CHUNK
 #define DGREP_FILTER_CHUNK 4096
 #endif
@@ -257,6 +265,14 @@ struct StepWide {
     s2 = one(s1, p.c2);
     s3 = one(s2, p.c3);
   }
+  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return one(s, p.c0); }
+  __device__ __forceinline__ void rest(const Pre& p, uint32_t f, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                       uint32_t& s3) const {
+    s0 = f;
+    s1 = one(s0, p.c1);
+    s2 = one(s1, p.c2);
+    s3 = one(s2, p.c3);
+  }
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return one(s, cls[b]); }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
 };
@@ -312,6 +328,15 @@ struct StepPair {
     s0 = s1;
     s2 = s3;
   }
+  // apply() in two parts: the word's first chain read, then the rest
+  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return t2(s + p.a0 + p.b1); }
+  __device__ __forceinline__ void rest(const Pre& p, uint32_t f, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                       uint32_t& s3) const {
+    s1 = f;
+    s3 = t2(s1 + p.a2 + p.b3);
+    s0 = s1;
+    s2 = s3;
+  }
   // single-byte step (rare paths): state id = (premultiplied state - kPairT2) / row bytes
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
     return T1[((s - kPairT2) / div) * K + (ub(b) >> 1)];
@@ -361,6 +386,14 @@ struct StepFilter {
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
     s0 = one(s, p.c0);
+    s1 = one(s0, p.c1);
+    s2 = one(s1, p.c2);
+    s3 = one(s2, p.c3);
+  }
+  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return one(s, p.c0); }
+  __device__ __forceinline__ void rest(const Pre& p, uint32_t f, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                       uint32_t& s3) const {
+    s0 = f;
     s1 = one(s0, p.c1);
     s2 = one(s1, p.c2);
     s3 = one(s2, p.c3);
@@ -562,24 +595,30 @@ struct Emitter {
 struct Blk {
   uint64_t pos;     // block start
   bool past;        // block lies at or beyond the chunk end
-  uint32_t nl0;     // r.nl at block start
-  uint32_t nlrun;   // '\n' in the words processed so far
-  uint32_t lnl;     // last '\n' of the words processed so far, 8 * (block offset + 3); 0: none yet
+  uint32_t nlrun;   // '\n' consumed by the lane so far (r.nl at block start + this block's)
+  uint32_t lnl;     // the line the next byte belongs to, encoded (lnl_update); 0: not owned
 };
-// Block-relative position of the last '\n', kept as ONE register per block:
-// for word J with newline mask m, f = sat(K_J - ffbh(m)) with K_J = 32 J + 48
-// is 8 * (4 J + k + 3) for its last '\n' at byte k (ffbh = 24 - 8 k) and 0 for a
-// word without one (ffbh(0) = ~0u saturates), so lnl = max(lnl, f): three VALU
-// per word (as the mask + word index pair took), and the matching-line path
-// reads the line start with one shift instead of rebuilding it from the pair.
+// Where the current line started, as ONE register per block: lnl = 8 * (q + 3 +
+// kLnlOff) for the last '\n' seen at block offset q. Word J with newline mask m
+// gives f = sat(K_J - ffbh(m)), K_J = 32 J + 48 + 8 kLnlOff: 8 * (4 J + k + 3 +
+// kLnlOff) for its last '\n' at byte k (ffbh = 24 - 8 k), 0 for a word without
+// one (ffbh(0) = ~0u saturates); lnl = max(lnl, f) -- three VALU per word. A
+// block inside the chunk starts from the lane's previous '\n' (q < 0, a value
+// below every in-block one), so the matching-line path reads the line start
+// with one shift and "the lane owns the line" is lnl != 0 (0: the lane has not
+// crossed a '\n' yet). Blocks past the chunk end start from kLnlSeen (owned,
+// previous '\n' in r.prev_nl: q there may lie further back than kLnlOff).
+constexpr uint32_t kLnlOff = 1u << 17;  // > 2 * 32 KiB: any q >= -(C + 1) inside the chunk
+constexpr uint32_t kLnlBase = 8u * (3u + kLnlOff);  // lnl >= kLnlBase: a '\n' inside this block
+constexpr uint32_t kLnlSeen = 8u;
 template <int J>
 __device__ __forceinline__ uint32_t lnl_update(uint32_t lnl, uint32_t m) {
   uint32_t t;
   asm("v_ffbh_u32 %0, %1" : "=v"(t) : "v"(m));
-  return max(lnl, __builtin_elementwise_sub_sat(uint32_t(32 * J + 48), t));
+  return max(lnl, __builtin_elementwise_sub_sat(uint32_t(32 * J + 48) + 8u * kLnlOff, t));
 }
-// block offset of the '\n' that lnl (!= 0) records
-__device__ __forceinline__ uint32_t lnl_pos(uint32_t lnl) { return (lnl >> 3) - 3u; }
+// block offset of the '\n' that lnl (>= kLnlBase) records
+__device__ __forceinline__ uint32_t lnl_pos(uint32_t lnl) { return (lnl >> 3) - (3u + kLnlOff); }
 
 // the steppers whose lanes carry the dummy slot (slot_stride): one stream per lane
 template <class Step, bool DIRECT>
@@ -595,21 +634,40 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit);
 
-template <int J, bool MAP, class Step, int E, bool DIRECT>
+// The steppers whose chain is LDS reads (pair, filter): issue the word's first
+// chain read BEFORE the next word's class reads (`pf`). LDS reads complete in
+// order, so a chain read issued after them also waits for them.
+template <class Step>
+constexpr bool chain_first() {
+  return DGREP_CHAIN_FIRST && (Step::kKind == kStepPair || Step::kKind == kStepFilter);
+}
+// sched_barrier mask: everything but LDS instructions may cross
+constexpr int kSchedNoDs = 0x7f;
+
+template <int J, bool MAP, class Step, int E, bool DIRECT, class PF>
 __device__ __forceinline__ void word_step(const Step& st, uint32_t M, uint32_t x, const typename Step::Pre& pre,
                                           uint32_t& s, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit,
-                                          uint32_t& mlo, uint32_t& mhi) {
+                                          uint32_t& mlo, uint32_t& mhi, PF&& pf) {
+  if constexpr (!chain_first<Step>()) pf();
   // StepTable: keep each word's work in place (hoisting the chain-independent
   // newline masks of a whole block costs ~100 VGPRs). StepSheng8 wants the
   // opposite: its state-independent LDS reads should run ahead of the chain.
   if (Step::kKind != kStepSheng8 && Step::kKind != kStepPair) __builtin_amdgcn_sched_barrier(0);
   const uint32_t m = nl_mask(x);
   uint32_t s0, s1, s2, s3;
-  st.apply(pre, s, s0, s1, s2, s3);
+  if constexpr (chain_first<Step>()) {
+    const uint32_t f = st.first(pre, s);
+    __builtin_amdgcn_sched_barrier(kSchedNoDs);
+    pf();
+    __builtin_amdgcn_sched_barrier(kSchedNoDs);
+    st.rest(pre, f, s0, s1, s2, s3);
+  } else {
+    st.apply(pre, s, s0, s1, s2, s3);
+  }
   if constexpr (MAP) {
     // Sheng chunk map: every state at once (two v_perm per byte), up to and
     // including the chunk's first '\n', whose offset completes the record
-    if (!b.past && b.nl0 + b.nlrun == 0u) {
+    if (!b.past && b.nlrun == 0u) {
       const uint32_t k = m ? uint32_t(__builtin_ctz(m)) >> 3 : 3u;
       st.compose(pre, k, mlo, mhi);
       if (m) *emit.cmap = make_uint4(mlo, mhi, uint32_t(b.pos) + 4u * J + k, 0u);
@@ -665,20 +723,21 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
   if (!b.past && (m & (m - 1u)) == 0u) {
     // branch-free operands (selects, no nested exec-mask regions)
     const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
-    // the line starts after the block's last '\n' so far, else after r.prev_nl
-    const uint32_t start = b.lnl ? uint32_t(b.pos) + (b.lnl >> 3) - 2u : uint32_t(r.prev_nl) + 1u;
+    // the line starts one byte after the '\n' lnl records (inside the chunk,
+    // lnl also encodes r.prev_nl: see lnl_update)
+    const uint32_t start = uint32_t(b.pos) + (b.lnl >> 3) - (2u + kLnlOff);
     const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
     if constexpr (flat_emit<Step, DIRECT>())
-      emit.inner_flat(r, uint32_t(b.pos) + 4u * J + k, start, b.nl0 + b.nlrun, cand_of(st, sk),
-                      r.seen | (b.lnl != 0));
-    else if (r.seen | (b.lnl != 0))
-      emit.inner(r, uint32_t(b.pos) + 4u * J + k, start, b.nl0 + b.nlrun, cand_of(st, sk));
+      emit.inner_flat(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, cand_of(st, sk), b.lnl != 0);
+    else if (b.lnl != 0)
+      emit.inner(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, cand_of(st, sk));
     return;
   }
   const uint64_t q0 = b.pos + 4u * J;
-  const bool seen_w = r.seen || b.lnl != 0;
-  const bool term_w = r.term || (b.past && b.lnl != 0);
-  const int64_t prev_w = b.lnl ? int64_t(b.pos + lnl_pos(b.lnl)) : r.prev_nl;
+  const bool nl_w = b.lnl >= kLnlBase;  // a '\n' in an earlier word of this block
+  const bool seen_w = b.lnl != 0;
+  const bool term_w = r.term || (b.past && nl_w);
+  const int64_t prev_w = nl_w ? int64_t(b.pos + lnl_pos(b.lnl)) : r.prev_nl;
   uint32_t evm;
   if constexpr (Step::kKind == kStepPair)
     evm = st.evm(s1, s3);
@@ -694,7 +753,7 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
     if (!ok) continue;
     const int64_t start = below ? int64_t(q0 + hi_byte(below)) + 1 : prev_w + 1;
     const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
-    emit(r, q0 + k, start, b.nl0 + b.nlrun + uint32_t(__popc(below)), cand_of(st, sk));
+    emit(r, q0 + k, start, b.nlrun + uint32_t(__popc(below)), cand_of(st, sk));
   }
 }
 
@@ -709,22 +768,31 @@ template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
-  if (__builtin_expect(word_any(st, M, s0, s1, s2, s3), 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+  const bool ev = word_any(st, M, s0, s1, s2, s3);
+#if DGREP_EV_BALLOT
+  // wave-uniform skip first (v_cmp + s_cmp + s_cbranch in the common no-event
+  // word, instead of saving, clearing and restoring exec around an empty region)
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
+    if (ev) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+  }
+#else
+  if (__builtin_expect(ev, 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+#endif
   word_nl<J>(m, b);
 }
 
 __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const LaneRun& r) {
   b.pos = pos;
   b.past = pos >= C;
-  b.nl0 = r.nl;
-  b.nlrun = 0;
-  b.lnl = 0;
+  b.nlrun = r.nl;
+  // inside the chunk: r.prev_nl - pos >= -(C + 1) > -kLnlOff
+  b.lnl = !r.seen ? 0u : b.past ? kLnlSeen : 8u * uint32_t(int32_t(r.prev_nl - int64_t(pos)) + int32_t(3u + kLnlOff));
 }
 
 __device__ __forceinline__ void blk_finish(const Blk& b, uint32_t s, LaneRun& r) {
   r.s = s;
-  r.nl = b.nl0 + b.nlrun;
-  if (b.lnl) {
+  r.nl = b.nlrun;
+  if (b.lnl >= kLnlBase) {
     r.seen = true;
     r.prev_nl = int64_t(b.pos + lnl_pos(b.lnl));
     if (b.past) r.term = true;
@@ -798,8 +866,9 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
 #define DG_W(J)                                                                         \
   if ((J) < NW) {                                                                       \
     const typename Step::Pre cur = pre;                                                 \
-    if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : 0]);                     \
-    word_step<J, MAP>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit, mlo, mhi);      \
+    word_step<J, MAP>(st, M, w[(J) < NW ? (J) : 0], cur, s, b, r, emit, mlo, mhi, [&] { \
+      if ((J) + 1 < NW) pre = st.prep(w[(J) + 1 < NW ? (J) + 1 : 0]);                   \
+    });                                                                                 \
   }
   DG_W(0) DG_W(1) DG_W(2) DG_W(3) DG_W(4) DG_W(5) DG_W(6) DG_W(7)
   DG_W(8) DG_W(9) DG_W(10) DG_W(11) DG_W(12) DG_W(13) DG_W(14) DG_W(15)
@@ -807,7 +876,7 @@ __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint
   DG_W(24) DG_W(25) DG_W(26) DG_W(27) DG_W(28) DG_W(29) DG_W(30) DG_W(31)
 #undef DG_W
   if constexpr (MAP) {
-    if (b.nl0 + b.nlrun == 0u) *emit.mapsl = make_uint2(mlo, mhi);
+    if (b.nlrun == 0u) *emit.mapsl = make_uint2(mlo, mhi);
   }
   blk_finish(b, s, r);
 }
@@ -1072,6 +1141,94 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// Calls f(byte) for every byte of [a, e), read in aligned 16-byte pieces (the
+// next piece is loaded while this one is stepped; the scan read the line long
+// ago, so its bytes come from HBM). f returns false to stop early.
+template <class F>
+__device__ __forceinline__ void for_line_bytes(const uint8_t* data, uint64_t a, uint64_t e, F&& f) {
+  if (a >= e) return;
+  uint4 nxt = *reinterpret_cast<const uint4*>(data + (a & ~uint64_t(15)));
+  for (uint64_t q = a & ~uint64_t(15); q < e; q += 16) {
+    const uint4 w = nxt;
+    if (q + 16 < e) nxt = *reinterpret_cast<const uint4*>(data + q + 16);
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    bool go = true;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t pos = q + uint64_t(j);
+      if (go && pos >= a && pos < e) go = f((ws[j >> 2] >> (8 * (j & 3))) & 0xffu);
+    }
+    if (!go) return;
+  }
+}
+
+// ---- in-kernel candidate verification (kStepFilter, exact DFA) -------------
+// The tile's candidate lines are decided by the lane that owns them right after
+// its chunk, before the tile's records are counted: no verification pass, no
+// compaction, and the ordering passes are queued behind the scan as for the
+// other steppers. A candidate line left the LDS image at some byte: it is
+// re-walked on the image (LDS) up to there, then on the whole DFA (HBM/L2, one
+// dependent load per byte) -- grep.go:21 on that line.
+__device__ __forceinline__ uint32_t vfull_next(const ScanArgs& a, uint32_t s, uint32_t c) {
+  const size_t i = size_t(s) * a.nclasses + c;
+  return a.vfull_u32 ? static_cast<const uint32_t*>(a.vfull)[i] : uint32_t(static_cast<const uint16_t*>(a.vfull)[i]);
+}
+__device__ __forceinline__ bool filter_line_matches(const ScanArgs& a, const StepFilter& st, uint64_t p, uint64_t len) {
+  const uint32_t K = a.nclasses;
+  const uint32_t cand = a.cand_end - 2u * K;  // image ids: ..., CAND, start_m, CAND_END
+  uint32_t ps = a.start;                      // image state (premultiplied) while on the image
+  uint32_t fs = 0;                            // whole-DFA state once deep
+  bool deep = false;
+  for_line_bytes(a.data, p, p + len, [&](uint32_t b) {
+    const uint32_t c = st.cls(b);
+    if (!deep) {
+      const uint32_t nps = st.one(ps, c);
+      if (nps == cand) {
+        fs = vfull_next(a, a.vmap[ps / K], c);
+        deep = true;
+      } else {
+        ps = nps;
+      }
+    } else {
+      fs = vfull_next(a, fs, c);
+    }
+    return !deep || fs != a.vmatched;  // the absorbing accepting state decides the line
+  });
+  const uint32_t cn = st.cls(uint32_t('\n'));
+  return deep ? vfull_next(a, fs, cn) == a.vstart_m : st.one(ps, cn) == a.start_m;
+}
+// The lane's records (LDS slots, then its spill area) with every candidate
+// decided: kept ones are compacted in place, r.nev becomes their count. A lane
+// whose records overflowed its slots + spill keeps them for the overflow pass
+// (verify_kernel then decides those candidates).
+template <int E>
+__device__ __forceinline__ void filter_verify_lane(const ScanArgs& a, const StepFilter& st, uint64_t cs, LaneRun& r,
+                                                   uint32_t* slots, uint2* spill, uint32_t spill_cap,
+                                                   const uint64_t* tail) {
+  const uint32_t nev = r.nev;
+  if (nev > uint32_t(E) + spill_cap) return;
+  uint32_t kept = 0;
+  for (uint32_t j = 0; j < nev; ++j) {
+    uint2 w = j < uint32_t(E) ? make_uint2(slots[2 * j], slots[2 * j + 1]) : spill[j - uint32_t(E)];
+    bool keep = true;
+    if (w.y & kCandidateBit) {
+      w.y &= ~kCandidateBit;
+      const uint64_t len = w.y == kSlotLong ? *tail : uint64_t(w.y);
+      keep = filter_line_matches(a, st, cs + (w.x & 0xffffu), len);
+    }
+    if (keep) {
+      if (kept < uint32_t(E)) {
+        slots[2 * kept] = w.x;
+        slots[2 * kept + 1] = w.y;
+      } else {
+        spill[kept - uint32_t(E)] = w;
+      }
+      ++kept;
+    }
+  }
+  r.nev = kept;
+}
+
 // waves per SIMD the register allocation must leave room for
 template <class Step>
 constexpr int waves_per_simd() {
@@ -1137,6 +1294,15 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         em.spill_cap = a.spill_per_lane;
       }
       nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
+      if constexpr (Step::kKind == kStepFilter) {
+        if (a.vfull) {
+          const uint32_t nev0 = r[0].nev;
+          filter_verify_lane<E>(a, st, cs[0], r[0], slots, em.spill, em.spill_cap, tails);
+          // dropped candidates, for dgrep_last_scan_stats (counter 3)
+          const uint32_t drop = __shfl(wave_incl_scan(nev0 - r[0].nev), 63, 64);
+          if (lane == 0 && drop) atomicAdd(a.counter + 3, (unsigned long long)drop);
+        }
+      }
     }
     if constexpr (track_long<Step, false>()) {
       // '\n' per chunk (chunk index = t * 64 S + 64 k + lane): where the long-line
@@ -1324,27 +1490,6 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
       v.tiles[t].count = kept;
       atomicAdd(v.removed, (unsigned long long)(ti.count - kept));
     }
-  }
-}
-
-// Calls f(byte) for every byte of [a, e), read in aligned 16-byte pieces (the
-// next piece is loaded while this one is stepped; the scan read the line long
-// ago, so its bytes come from HBM). f returns false to stop early.
-template <class F>
-__device__ __forceinline__ void for_line_bytes(const uint8_t* data, uint64_t a, uint64_t e, F&& f) {
-  if (a >= e) return;
-  uint4 nxt = *reinterpret_cast<const uint4*>(data + (a & ~uint64_t(15)));
-  for (uint64_t q = a & ~uint64_t(15); q < e; q += 16) {
-    const uint4 w = nxt;
-    if (q + 16 < e) nxt = *reinterpret_cast<const uint4*>(data + q + 16);
-    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-    bool go = true;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint64_t pos = q + uint64_t(j);
-      if (go && pos >= a && pos < e) go = f((ws[j >> 2] >> (8 * (j & 3))) & 0xffu);
-    }
-    if (!go) return;
   }
 }
 

@@ -454,6 +454,29 @@ def test_filter_candidates_dense_and_long(filter_ctx):
             assert st["stepper"] == "filter", st
 
 
+def test_filter_in_kernel_verification_with_overflow(filter_ctx):
+    """Exact filter DFA (4 LDS rows, so nearly every line is a candidate): the
+    scan kernel decides its lanes' candidates itself; lanes whose records
+    overflow their slots + spill go through the overflow pass and leave their
+    candidates to verify_kernel. Both in one scan, bit-exact vs the oracle."""
+    filter_ctx.set_stepper("filter", 4)
+    try:
+        filter_ctx.set_lane_chunk(4096)
+        # 4-7 B lines: ~750 per 4 KiB lane chunk (> 4 slots + 240 spill records)
+        # in the dense part, longer lines after it (lanes that verify in-kernel)
+        rnd = random.Random(7)
+        data = b"\n".join(b"ab " + b"x" * rnd.randrange(4) for _ in range(60000)) + b"\n" + b"\n".join(
+            b"noise line %d: a b, ab xx, the pattern or not" % i for i in range(20000))
+        for pattern in (b"ab x{3}", b"^ab x?$", b"b xx"):
+            _check(filter_ctx, pattern, data, threads=16)
+            st = filter_ctx.scan_stats()
+            assert st["stepper"] == "filter", st
+            assert st["overflow_lanes"] > 0, st
+            assert st["candidates"] > 0, st  # dropped, in the kernel or by verify_kernel
+    finally:
+        filter_ctx.set_lane_chunk(0)
+
+
 # ---- the pair stepper (two bytes per LDS lookup, shadow states) -------------
 PAIR_PATTERNS = [b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"(WARN|ERROR) [a-z_]+",
                  b"timeout while waiting for lock", b"\\bkey\\b", b"^[ -~]{45}$", b"e(r|x)+o", b"a|^$",
