@@ -114,15 +114,6 @@ struct ScanArgs {
   unsigned long long* pend_count;
   // Sheng stepper: the chunk maps instead of chunk_nl (nullptr: none)
   ChunkMap* chunk_map;
-  // kStepFilter, exact DFA: candidates are decided in the scan kernel at the
-  // tile's end (filter_line_matches) on the whole DFA (vfull: breadth-first ids,
-  // u16 entries, u32 if vfull_u32); vmap = image state id -> vfull id for the
-  // image's kept states. nullptr: decided afterwards by verify_kernel.
-  const void* vfull;
-  const uint32_t* vmap;
-  uint32_t vfull_u32;
-  uint32_t vstart_m;  // start_m in vfull ids
-  uint32_t vmatched;  // the absorbing accepting state in vfull ids (UINT32_MAX: none)
 };
 
 // the long-line kernels' arguments (long_end / long_map / long_fin)

@@ -104,14 +104,6 @@
 #define DGREP_PAIR_WAVES 3
 #endif
 // Filter (C4, > 256 states): one 1024-thread workgroup per CU shares one LDS image
-// pair / filter: the word's first chain read before the next word's class reads
-#ifndef DGREP_CHAIN_FIRST
-#define DGREP_CHAIN_FIRST 0
-#endif
-// word_events: skip the matching-line region with a wave-uniform branch
-#ifndef DGREP_EV_BALLOT
-#define DGREP_EV_BALLOT 0
-#endif
 #ifndef DGREP_FILTER_CHUNK
 #define DGREP_FILTER_CHUNK 4096
 #endif
@@ -634,12 +626,13 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit);
 
-// The steppers whose chain is LDS reads (pair, filter): issue the word's first
-// chain read BEFORE the next word's class reads (`pf`). LDS reads complete in
-// order, so a chain read issued after them also waits for them.
+// Filter (four dependent LDS reads per word): issue the word's first chain
+// read BEFORE the next word's class reads (`pf`). LDS reads complete in order,
+// so a chain read issued after them also waits for them. Same-box A/B: C4
+// kernel 3,678 -> 3,773 GB/s; the pair stepper (C3) lost 2.6 % with it.
 template <class Step>
 constexpr bool chain_first() {
-  return DGREP_CHAIN_FIRST && (Step::kKind == kStepPair || Step::kKind == kStepFilter);
+  return Step::kKind == kStepFilter;
 }
 // sched_barrier mask: everything but LDS instructions may cross
 constexpr int kSchedNoDs = 0x7f;
@@ -768,16 +761,7 @@ template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
-  const bool ev = word_any(st, M, s0, s1, s2, s3);
-#if DGREP_EV_BALLOT
-  // wave-uniform skip first (v_cmp + s_cmp + s_cbranch in the common no-event
-  // word, instead of saving, clearing and restoring exec around an empty region)
-  if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
-    if (ev) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
-  }
-#else
-  if (__builtin_expect(ev, 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
-#endif
+  if (__builtin_expect(word_any(st, M, s0, s1, s2, s3), 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
   word_nl<J>(m, b);
 }
 
@@ -1162,73 +1146,6 @@ __device__ __forceinline__ void for_line_bytes(const uint8_t* data, uint64_t a, 
   }
 }
 
-// ---- in-kernel candidate verification (kStepFilter, exact DFA) -------------
-// The tile's candidate lines are decided by the lane that owns them right after
-// its chunk, before the tile's records are counted: no verification pass, no
-// compaction, and the ordering passes are queued behind the scan as for the
-// other steppers. A candidate line left the LDS image at some byte: it is
-// re-walked on the image (LDS) up to there, then on the whole DFA (HBM/L2, one
-// dependent load per byte) -- grep.go:21 on that line.
-__device__ __forceinline__ uint32_t vfull_next(const ScanArgs& a, uint32_t s, uint32_t c) {
-  const size_t i = size_t(s) * a.nclasses + c;
-  return a.vfull_u32 ? static_cast<const uint32_t*>(a.vfull)[i] : uint32_t(static_cast<const uint16_t*>(a.vfull)[i]);
-}
-__device__ __forceinline__ bool filter_line_matches(const ScanArgs& a, const StepFilter& st, uint64_t p, uint64_t len) {
-  const uint32_t K = a.nclasses;
-  const uint32_t cand = a.cand_end - 2u * K;  // image ids: ..., CAND, start_m, CAND_END
-  uint32_t ps = a.start;                      // image state (premultiplied) while on the image
-  uint32_t fs = 0;                            // whole-DFA state once deep
-  bool deep = false;
-  for_line_bytes(a.data, p, p + len, [&](uint32_t b) {
-    const uint32_t c = st.cls(b);
-    if (!deep) {
-      const uint32_t nps = st.one(ps, c);
-      if (nps == cand) {
-        fs = vfull_next(a, a.vmap[ps / K], c);
-        deep = true;
-      } else {
-        ps = nps;
-      }
-    } else {
-      fs = vfull_next(a, fs, c);
-    }
-    return !deep || fs != a.vmatched;  // the absorbing accepting state decides the line
-  });
-  const uint32_t cn = st.cls(uint32_t('\n'));
-  return deep ? vfull_next(a, fs, cn) == a.vstart_m : st.one(ps, cn) == a.start_m;
-}
-// The lane's records (LDS slots, then its spill area) with every candidate
-// decided: kept ones are compacted in place, r.nev becomes their count. A lane
-// whose records overflowed its slots + spill keeps them for the overflow pass
-// (verify_kernel then decides those candidates).
-template <int E>
-__device__ __forceinline__ void filter_verify_lane(const ScanArgs& a, const StepFilter& st, uint64_t cs, LaneRun& r,
-                                                   uint32_t* slots, uint2* spill, uint32_t spill_cap,
-                                                   const uint64_t* tail) {
-  const uint32_t nev = r.nev;
-  if (nev > uint32_t(E) + spill_cap) return;
-  uint32_t kept = 0;
-  for (uint32_t j = 0; j < nev; ++j) {
-    uint2 w = j < uint32_t(E) ? make_uint2(slots[2 * j], slots[2 * j + 1]) : spill[j - uint32_t(E)];
-    bool keep = true;
-    if (w.y & kCandidateBit) {
-      w.y &= ~kCandidateBit;
-      const uint64_t len = w.y == kSlotLong ? *tail : uint64_t(w.y);
-      keep = filter_line_matches(a, st, cs + (w.x & 0xffffu), len);
-    }
-    if (keep) {
-      if (kept < uint32_t(E)) {
-        slots[2 * kept] = w.x;
-        slots[2 * kept + 1] = w.y;
-      } else {
-        spill[kept - uint32_t(E)] = w;
-      }
-      ++kept;
-    }
-  }
-  r.nev = kept;
-}
-
 // waves per SIMD the register allocation must leave room for
 template <class Step>
 constexpr int waves_per_simd() {
@@ -1294,15 +1211,6 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         em.spill_cap = a.spill_per_lane;
       }
       nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
-      if constexpr (Step::kKind == kStepFilter) {
-        if (a.vfull) {
-          const uint32_t nev0 = r[0].nev;
-          filter_verify_lane<E>(a, st, cs[0], r[0], slots, em.spill, em.spill_cap, tails);
-          // dropped candidates, for dgrep_last_scan_stats (counter 3)
-          const uint32_t drop = __shfl(wave_incl_scan(nev0 - r[0].nev), 63, 64);
-          if (lane == 0 && drop) atomicAdd(a.counter + 3, (unsigned long long)drop);
-        }
-      }
     }
     if constexpr (track_long<Step, false>()) {
       // '\n' per chunk (chunk index = t * 64 S + 64 k + lane): where the long-line

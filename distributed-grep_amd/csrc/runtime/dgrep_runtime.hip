@@ -96,7 +96,6 @@ struct dgrep_ctx {
   uint32_t blob_start = 0, blob_start_m = 0;  // start / start_m in d_full's (breadth-first) ids
   uint32_t blob_matched = UINT32_MAX;          // the absorbing accepting state in d_full's ids (none: UINT32_MAX)
   uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
-  uint32_t* d_vmap = nullptr;  // filter image id -> d_full id (in-kernel verification; nullptr: none)
   uint32_t* d_nfa = nullptr;                   // DGREP_DFA_PARTIAL: the NFA program (verify_nfa_kernel)
   uint32_t nfa_words = 0;                      // its position-set words
   int blocks_per_cu = 1;
@@ -290,11 +289,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
 // if not even start, start_m and their successors fit.
 // `excluded`: a partial blob's CAND state (never kept, so every transition
 // into it is a filter CAND too).
-// `kept`: blob state of each image id below CAND (the states a line walks
-// through before it leaves the image).
 bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint32_t row_cap, std::vector<uint8_t>* img,
-                        uint32_t* start, uint32_t* start_m, uint32_t* cand_end, std::vector<uint32_t>* kept,
-                        uint32_t excluded = UINT32_MAX) {
+                        uint32_t* start, uint32_t* start_m, uint32_t* cand_end, uint32_t excluded = UINT32_MAX) {
   const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
   const uint32_t cn = h.byte_class[uint8_t('\n')];
   // rows that fit (row_cap: dgrep_set_stepper's test knob)
@@ -314,12 +310,8 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
   if (keep < 2) return false;
   std::vector<uint32_t> id(S, UINT32_MAX);
   uint32_t next = 0;
-  kept->clear();
   for (uint32_t i = 0; i < keep; ++i)
-    if (order[i] != M) {
-      id[order[i]] = next++;
-      kept->push_back(order[i]);
-    }
+    if (order[i] != M) id[order[i]] = next++;
   const bool exact = keep == S && !part;  // the whole DFA fits: no candidates
   const uint32_t CAND = exact ? UINT32_MAX : next++;
   id[M] = next++;
@@ -402,7 +394,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_vmap, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
                   c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
@@ -488,11 +480,10 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     return DGREP_E_UNSUPPORTED;
   }
   std::vector<uint8_t> filter_img;
-  std::vector<uint32_t> f_kept;
   uint32_t f_start = 0, f_m = 0, f_cend = UINT32_MAX;
   const bool filter_ok = !pair_ok && ((force == 0 && (h.nstates > 256 || partial)) || force == 4) &&
                          build_filter_image(h, trans, c->wide_hot_rows_cap, &filter_img, &f_start, &f_m, &f_cend,
-                                            &f_kept, partial ? h.nstates - 1 : UINT32_MAX);
+                                            partial ? h.nstates - 1 : UINT32_MAX);
   if ((force == 4 || partial) && !filter_ok) {
     c->err = "dgrep_load_dfa: the filter stepper cannot hold this DFA's first states";
     return DGREP_E_UNSUPPORTED;
@@ -516,8 +507,6 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_nfa = nullptr;
   if (c->d_full) HIPCHK(hipFree(c->d_full));
   c->d_full = nullptr;
-  if (c->d_vmap) HIPCHK(hipFree(c->d_vmap));
-  c->d_vmap = nullptr;
   if (pair_ok) {
     // image built above
   } else if (filter_ok && partial) {
@@ -569,14 +558,6 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
       for (uint32_t k = 0; k < K && absorbing; ++k)
         if (k != cn && trans[size_t(x) * K + k] != x) absorbing = false;
       if (absorbing) c->blob_matched = bid[x];
-    }
-    // the scan kernel decides the candidates itself (in-kernel verification):
-    // image id -> breadth-first id of the kept states
-    if (c->cand_end != UINT32_MAX) {
-      std::vector<uint32_t> vmap(f_kept.size());
-      for (size_t i = 0; i < f_kept.size(); ++i) vmap[i] = bid[f_kept[i]];
-      HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_vmap), vmap.size() * 4));
-      HIPCHK(hipMemcpy(c->d_vmap, vmap.data(), vmap.size() * 4, hipMemcpyHostToDevice));
     }
   } else if (h.nstates > 256 || force == 1) {
     if (h.nstates > 65535) {
@@ -830,15 +811,6 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.pair_thr = c->pair_args.thr;
   a.pair_div = c->pair_args.div;
   a.cand_end = c->cand_end;
-  // exact filter DFA: the scan decides its candidates (in-kernel verification)
-  const bool fused = filt && c->d_vmap != nullptr;
-  if (fused) {
-    a.vfull = c->d_full;
-    a.vmap = c->d_vmap;
-    a.vfull_u32 = c->full_u32 ? 1u : 0u;
-    a.vstart_m = c->blob_start_m;
-    a.vmatched = c->blob_matched;
-  }
   a.spill = use_spill ? c->d_spill : nullptr;
   a.spill_per_lane = use_spill ? DGREP_SPILL_RECORDS : 0;
   // every resident workgroup is launched even when the last round of tiles is
@@ -856,7 +828,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   // and never write past `capacity`) and the counters are read back after them.
   // Anything else shows in the counters, and the ordering is queued again once
   // the extra passes have run.
-  const bool speculate = (!filt || fused) && capacity != 0;
+  const bool speculate = !filt && capacity != 0;
   for (int attempt = 0; attempt < 3; ++attempt) {
     a.staging = c->d_staging;
     a.capacity = c->staging_cap;
@@ -904,12 +876,8 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     HIPCHK(hipEventRecord(c->ev3, c->stream));
   }
   uint64_t total = staged;
-  // candidates the scan kernel decided and dropped (in-kernel verification)
-  const uint64_t kdrop = fused ? ctr[3] : 0;
-  S.candidates = kdrop;
-  // verification pass: the partial-blob filter, candidates of lanes that went
-  // through the overflow pass (in-kernel verification skips them), parked lines
-  const bool verify = (filt && (!fused || over)) || npend;
+  // verification pass: the filter's candidates, parked long lines
+  const bool verify = filt || npend;
   if (verify && staged && staged <= a.capacity) {
     VerifyArgs v;
     v.data = d_data;
@@ -953,8 +921,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventElapsedTime(&S.verify_ms, c->ev4, c->ev5));
     c->last_ms += S.verify_ms;
-    // counters[3] already held the candidates the scan dropped itself (fused)
-    total = staged - (removed - kdrop);
+    total = staged - removed;
     S.candidates = removed;  // dropped ones; kept candidates count as matches
   }
   if (filt) c->staged_hint = staged;

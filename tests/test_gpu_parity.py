@@ -454,11 +454,11 @@ def test_filter_candidates_dense_and_long(filter_ctx):
             assert st["stepper"] == "filter", st
 
 
-def test_filter_in_kernel_verification_with_overflow(filter_ctx):
-    """Exact filter DFA (4 LDS rows, so nearly every line is a candidate): the
-    scan kernel decides its lanes' candidates itself; lanes whose records
-    overflow their slots + spill go through the overflow pass and leave their
-    candidates to verify_kernel. Both in one scan, bit-exact vs the oracle."""
+def test_filter_verification_with_overflow(filter_ctx):
+    """Filter with 4 LDS rows (nearly every line a candidate) and lanes whose
+    records overflow their slots + spill: candidates staged by the scan AND by
+    the overflow pass are decided by verify_kernel in one call, bit-exact vs
+    the oracle."""
     filter_ctx.set_stepper("filter", 4)
     try:
         filter_ctx.set_lane_chunk(4096)
