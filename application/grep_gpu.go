@@ -1,3 +1,5 @@
+//go:build dgrep_gpu
+
 // grep_gpu.go -- the drop-in grep plugin for bgilby59/distributed-grep with
 // the Map body on MI355X through libdgrep.so (include/dgrep.h).
 //
@@ -10,12 +12,23 @@
 // on the GPU (dgrep_scan replaces grep.go:17-24); the KeyValues are rebuilt on
 // the host exactly as grep.go:25-28 builds them.
 //
-// Build (in the reference tree, next to application/grep.go):
-//   go build -buildmode=plugin -o grep.so ./application
-// with this repository's include/ and distributed-grep_amd/libdgrep.so on the
-// cgo paths below. UNTESTED AS GO: there is no Go toolchain in this image or
-// on the GPU box; tests/abi_c/plugin_sequence.c runs the same call sequence
-// from C and is tested on the GPU (tests/test_abi_c.py).
+// It declares the same package-level names as application/grep.go (pattern,
+// Map, Reduce), so the two must never be compiled together. Either build
+// (from the reference tree's root, this file copied to application/):
+//   single file -- go ignores build constraints on files named on the command
+//   line, and grep.go is not named:
+//     go build -buildmode=plugin -o grep.so ./application/grep_gpu.go
+//   or the package with tags -- after adding the line
+//     //go:build !dgrep_gpu
+//   (and a blank line) at the top of application/grep.go:
+//     go build -tags dgrep_gpu -buildmode=plugin -o grep.so ./application
+// with this repository's include/ and libdgrep.so on the cgo paths:
+//     export CGO_CFLAGS="-I<repo>/include"
+//     export CGO_LDFLAGS="-L<repo>/distributed-grep_amd -Wl,-rpath,<repo>/distributed-grep_amd"
+// UNTESTED AS GO: there is no Go toolchain in this image or on the GPU box;
+// tests/test_go_plugin.py checks the build constraints and top-level names of
+// both files, and tests/abi_c/plugin_sequence.c runs the same call sequence
+// from C on the GPU (tests/test_abi_c.py).
 //
 // Intended departures from grep.go (fail-stop, never a silent CPU path): a
 // valid Go pattern outside the compiler's subset (DGREP_E_UNSUPPORTED /
@@ -30,8 +43,7 @@
 package main
 
 /*
-#cgo CFLAGS: -I${SRCDIR}/../include
-#cgo LDFLAGS: -L${SRCDIR}/../distributed-grep_amd -ldgrep -Wl,-rpath,${SRCDIR}/../distributed-grep_amd
+#cgo LDFLAGS: -ldgrep
 #include <stdlib.h>
 #include "dgrep.h"
 */
