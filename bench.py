@@ -99,6 +99,8 @@ def parse():
                     help="full verification stops (and says how far it got) after this much wall time")
     ap.add_argument("--verify-windows", type=int, default=6)
     ap.add_argument("--lane-chunk", type=int, default=0, help="tuning: force the Sheng/pair/filter lane chunk (0 = adaptive)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the N-rank report (gloo, oracle instead of the GPU scan; value null)")
     ap.add_argument("--pattern", default=None,
                     help="ablation only: scan the workload's split with this pattern instead (not a BASELINE config)")
     return ap.parse_args()
@@ -125,7 +127,7 @@ def launch_ranks(args):
     import torch
 
     have = torch.cuda.device_count()
-    if have < args.gpus:
+    if have < args.gpus and not args.dry_run:
         log("bench.py --gpus %d: only %d GPU(s) visible; refusing to report an N=%d line" % (args.gpus, have, have))
         return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
@@ -149,19 +151,22 @@ def main():
         log("bench.py --gpus must be >= 1")
         sys.exit(2)
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
-    import dgrep
-
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    if args.dry_run:
+        # CPU rehearsal of the N-rank line (gloo): no GPU is touched
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
     if args.workload is None:
         args.workload = "c2" if world == 1 else "c5"
     wl = WORKLOADS[args.workload]
@@ -169,6 +174,61 @@ def main():
     n = int(gib * (1 << 30))
     n -= n % 64
     pattern = args.pattern if args.pattern is not None else workload_pattern(wl)
+    seed = wl["seed"] + wl.get("rank_seed_step", 1000) * rank
+
+    m = (measure_dry if args.dry_run else measure_gpu)(args, wl, world, rank, local, dev, n, pattern, seed)
+    count = m["count"]
+
+    # ---- parity on the full split: every rank checks its own ----------------
+    verified = None
+    if args.dry_run:
+        verified = {"mode": "none (dry run: the records are the oracle's own)"}
+    elif args.verify == "full":
+        threads = verify_threads(world)
+        verified = verify_full(m["buf"], n, m["line"][:count], m["start"][:count], m["len"][:count], pattern,
+                               threads, args.verify_seconds)
+        if world > 1:
+            ok = torch.tensor([verified["records_checked"], int(verified["complete"])], dtype=torch.int64, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            verified["all_ranks_complete"] = bool(ok[1].item())
+    elif args.verify == "windows" and rank == 0 and args.verify_windows > 0:
+        verified = {"mode": "windows", "windows": verify_windows(m["buf"], n, m["line"][:count], m["start"][:count],
+                                                                 m["len"][:count], pattern, args.verify_windows,
+                                                                 wl.get("verify_window", 2 << 20))}
+
+    # ---- CPU comparators, on rank 0 while the other ranks wait ---------------
+    cpu = cpu_mt = cpu_workers = None
+    if world > 1:
+        dist.barrier()
+    if rank == 0 and not args.no_cpu_baseline:
+        if world == 1:
+            cpu = cpu_baseline(m["buf"], n, pattern, args.cpu_seconds)
+            cpu_mt = cpu_baseline_mt(m["buf"], n, pattern, args.cpu_seconds / 2)
+        else:
+            # the reference at N: coordinator + N Go workers, one file each on
+            # one core (map_reduce/worker.go:126-145, coordinator.go:312,329-333):
+            # N threads of the per-line-compile restatement, each on its own part
+            # of the split; and the compiled-once oracle on the node's CPU share
+            cpu_workers = cpu_baseline_workers(m["buf"], n, pattern, args.cpu_seconds, world)
+            cpu_mt = cpu_baseline_mt(m["buf"], n, pattern, args.cpu_seconds / 2, threads=node_threads(world))
+    if world > 1:
+        dist.barrier()
+
+    line = build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, cpu_mt, cpu_workers)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def measure_gpu(args, wl, world, rank, local, dev, n, pattern, seed):
+    """Generate the rank's split in HBM, then W untimed and K timed steps of
+    dgrep_scan_device (+ the record gather at N > 1), bracketed by a barrier and
+    a device synchronisation."""
+    import torch
+    import torch.distributed as dist
+
+    import dgrep
 
     ctx = dgrep.Context(local)
     if args.lane_chunk:
@@ -179,7 +239,6 @@ def main():
 
     t = time.time()
     buf = torch.empty(n + 64, dtype=torch.uint8, device=dev)
-    seed = wl["seed"] + wl.get("rank_seed_step", 1000) * rank
     ctx.synth(buf.data_ptr(), n, seed, wl["kind"])
     torch.cuda.synchronize(dev)
     log("rank %d: generated %.1f GiB split in %.1fs; DFA %d states x %d classes" %
@@ -216,46 +275,85 @@ def main():
     count = 0
     for _ in range(args.steps):
         count = step()
-        kms.append(ctx.last_kernel_ms())  # scan kernel + overflow pass, HIP events on the launch stream
+        kms.append(ctx.last_kernel_ms())  # scan kernel + overflow pass + verification, HIP events on the launch stream
         stats.append(ctx.scan_stats())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    return dict(buf=buf, line=line_t, start=start_t, len=len_t, count=count, kms=kms, stats=stats, elapsed=elapsed,
+                nstates=cp.nstates, nclasses=cp.nclasses, build=dgrep.build_info())
+
+
+def measure_dry(args, wl, world, rank, local, dev, n, pattern, seed):
+    """--dry-run: the same line on the CPU (gloo), for rehearsing the N-rank
+    report without a GPU. The split comes from the generator's host twin and
+    the "scan" is the oracle's Map (kernel times = its wall time): the numbers
+    are NOT a measurement of this framework and the line says so."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import dgrep
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    from dgrep.dist import gather_records
+
+    buf = torch.frombuffer(bytearray(dgrep.synth_corpus_host(n, seed, wl["kind"]) + bytes(64)), dtype=torch.uint8)
+    host = buf[:n].numpy()
+    kms, stats, count, res = [], [], 0, None
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        t = time.perf_counter()
+        ln, st, le = O.grep_map(pattern.encode(), host, threads=2)
+        kms.append((time.perf_counter() - t) * 1e3)
+        count = len(ln)
+        res = (torch.from_numpy(ln.astype(np.int64)), torch.from_numpy(st.astype(np.int64)),
+               torch.from_numpy(le.astype(np.int64)))
+        if world > 1:
+            gather_records(res[0], res[1], res[2], count, dst=0, split=seed)
+        stats.append(dict(stepper="oracle (dry run)", lane_chunk=0, overflow_ms=0.0, verify_ms=0.0,
+                          scan_ms=kms[-1], candidates=0, overflow_lanes=0, pending=0))
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    return dict(buf=buf, line=res[0], start=res[1], len=res[2], count=count, kms=kms, stats=stats, elapsed=elapsed,
+                nstates=0, nclasses=0, build=dgrep.build_info())
+
+
+def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, cpu_mt, cpu_workers):
+    """The JSON line (rank 0 prints it). Every rank takes part in the
+    reductions: wall time = max over ranks; the roofline comes from the SLOWEST
+    rank's kernel time (max over ranks of its mean), per GPU and for the node."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    count, kms, stats = m["count"], m["kms"], m["stats"]
+    alg = n + STAGED_LINE_BYTES * count
+    kern_ms, kern_med = float(np.mean(kms)), float(np.median(kms))
+    mine = torch.tensor([m["elapsed"], kern_ms, kern_med, float(alg), float(count)], dtype=torch.float64, device=dev)
+    if world > 1:
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per = torch.stack(allr).cpu().numpy()
+    else:
+        per = mine.cpu().numpy()[None, :]
+    elapsed = float(per[:, 0].max())
     ms_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed / 1e9
-    kern_ms = float(np.mean(kms))
-    kern_med = float(np.median(kms))
+    slow = int(per[:, 1].argmax())
+    kern_max = float(per[slow, 1])
+    achieved = float(per[slow, 3]) / (kern_max * 1e-3) / 1e9       # the slowest rank's own bytes / its time
+    agg = float(per[:, 3].sum()) / (kern_max * 1e-3) / 1e9          # all ranks' bytes / the slowest time
     st = stats[-1]
-    achieved = (n + STAGED_LINE_BYTES * count) / (kern_ms * 1e-3) / 1e9
-
-    # ---- parity on the full split: every rank checks its own ----------------
-    verified = None
-    if args.verify == "full":
-        threads = verify_threads(world)
-        verified = verify_full(buf, n, line_t[:count], start_t[:count], len_t[:count], pattern, threads,
-                               args.verify_seconds)
-        if world > 1:
-            ok = torch.tensor([verified["records_checked"], int(verified["complete"])], dtype=torch.int64, device=dev)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            verified["all_ranks_complete"] = bool(ok[1].item())
-    elif args.verify == "windows" and rank == 0 and args.verify_windows > 0:
-        verified = {"mode": "windows", "windows": verify_windows(buf, n, line_t[:count], start_t[:count],
-                                                                 len_t[:count], pattern, args.verify_windows,
-                                                                 wl.get("verify_window", 2 << 20))}
-
-    cpu = cpu_mt = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(buf, n, pattern, args.cpu_seconds)
-        cpu_mt = cpu_baseline_mt(buf, n, pattern, args.cpu_seconds / 2)
 
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and not args.dry_run:
         try:
             with open(tpath) as f:
                 tr = json.load(f).get(args.workload)
@@ -263,67 +361,77 @@ def main():
                 traffic = tr.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-
-    if rank == 0:
-        out = {
-            "metric": "GB/s text scanned per GPU and whole node (1/2/4/8×MI355X), % of HBM peak",
-            "value": round(value, 2),
+    if rank != 0:
+        return None
+    counts = [int(c) for c in per[:, 4]]
+    out = {
+        "metric": "GB/s text scanned per GPU and whole node (1/2/4/8×MI355X), % of HBM peak",
+        "value": round(value, 2) if not args.dry_run else None,
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded log corpus generated in HBM, SURVEY.md §8d)",
+        "config": {
+            "workload": (wl["desc"] if world == 1 else wl["desc"] + "; one split per GPU + RCCL gather of match records to rank 0")
+                        + ("" if args.pattern is None else "; ABLATION: pattern overridden"),
+            "pattern": pattern if len(pattern) < 200 else pattern[:120] + "...(%d bytes)" % len(pattern),
+            "split_bytes_per_gpu": n,
+            "total_bytes": n * world,
+            "matching_lines_per_split": counts[0] if world == 1 else counts,
+            "dfa_states": m["nstates"],
+            "dfa_byte_classes": m["nclasses"],
+            "parallelism": "1 split per GPU x %d" % world,
+            "per_gpu_gbs": round(value / world, 2),
+            "hbm_frac_whole_node": round(value / (HBM_PEAK_GBS * world), 4),
+            "verified": verified,
+            "seed": seed,
+            "stepper": st["stepper"],
+            "lane_chunk": st["lane_chunk"],
+            "build": m["build"].split()[0][len("head="):],
+            "build_info": m["build"],
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "dgrep::scan_dfa8_kernel",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (seeded log corpus generated in HBM, SURVEY.md §8d)",
-            "config": {
-                "workload": (wl["desc"] if world == 1 else wl["desc"] + "; one split per GPU + RCCL gather of match records to rank 0")
-                            + ("" if args.pattern is None else "; ABLATION: pattern overridden"),
-                "pattern": pattern if len(pattern) < 200 else pattern[:120] + "...(%d bytes)" % len(pattern),
-                "split_bytes_per_gpu": n,
-                "total_bytes": n * world,
-                "matching_lines_per_split": int(count),
-                "dfa_states": cp.nstates,
-                "dfa_byte_classes": cp.nclasses,
-                "parallelism": "1 split per GPU x %d" % world,
-                "per_gpu_gbs": round(value / world, 2),
-                "hbm_frac_whole_node": round(value / (HBM_PEAK_GBS * world), 4),
-                "verified": verified,
-                "seed": seed,
-                "stepper": st["stepper"],
-                "lane_chunk": st["lane_chunk"],
-                "build": dgrep.build_info().split()[0][len("head="):],
-                "build_info": dgrep.build_info(),
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "dgrep::scan_dfa8_kernel",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel_ms_avg": round(kern_ms, 4),
-                "kernel_ms_median": round(kern_med, 4),
-                "kernel_ms_min": round(float(np.min(kms)), 4),
-                "overflow_ms_avg": round(float(np.mean([x["overflow_ms"] for x in stats])), 4),
-                "verify_ms_avg": round(float(np.mean([x["verify_ms"] for x in stats])), 4),
-                "scan_ms_avg": round(float(np.mean([x["scan_ms"] for x in stats])), 4),
-                "candidates_dropped": int(st["candidates"]),
-                "overflow_lanes": int(st["overflow_lanes"]),
-                "pending_lines": int(st["pending"]),
-                "timing": "HIP events on the launch stream around the scan kernel, the overflow pass and (filter "
-                          "stepper) the candidate verification (dgrep_last_kernel_ms), averaged over the timed steps",
-                "algorithmic_bytes_per_launch": int(n + STAGED_LINE_BYTES * count),
-            },
-            "cpu_baseline": cpu,
-            "cpu_baseline_mt": cpu_mt,
-        }
-        print(json.dumps(out), flush=True)
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel_ms_avg": round(kern_max, 4),
+            "kernel_ms_median": round(float(per[slow, 2]), 4),
+            "kernel_ms_min": round(float(np.min(kms)), 4),
+            "per_rank_kernel_ms_avg": [round(float(x), 4) for x in per[:, 1]],
+            "slowest_rank": slow,
+            "aggregate": {"achieved": round(agg, 2), "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                          "frac": round(agg / (HBM_PEAK_GBS * world), 4),
+                          "note": "all ranks' algorithmic bytes / the slowest rank's mean kernel time"},
+            "overflow_ms_avg": round(float(np.mean([x["overflow_ms"] for x in stats])), 4),
+            "verify_ms_avg": round(float(np.mean([x["verify_ms"] for x in stats])), 4),
+            "scan_ms_avg": round(float(np.mean([x["scan_ms"] for x in stats])), 4),
+            "candidates_dropped": int(st["candidates"]),
+            "overflow_lanes": int(st["overflow_lanes"]),
+            "pending_lines": int(st["pending"]),
+            "timing": "HIP events on the launch stream around the scan kernel, the overflow pass and the "
+                      "verification / long-line resolution (dgrep_last_kernel_ms), averaged over the timed steps; "
+                      "at N > 1 the slowest rank's average (kernel_ms_avg) prices `achieved`",
+            "algorithmic_bytes_per_launch": int(per[slow, 3]),
+        },
+        "cpu_baseline": cpu,
+        "cpu_baseline_mt": cpu_mt,
+    }
     if world > 1:
-        dist.destroy_process_group()
+        out["cpu_baseline_workers"] = cpu_workers
+    if args.dry_run:
+        out["dry_run"] = ("CPU rehearsal (gloo): the split is scanned by the oracle, not by the GPU; "
+                          "value is null and no number here measures this framework")
+    return out
 
 
 def last_newline(host):
@@ -501,11 +609,71 @@ def cpu_baseline(buf, n, pattern, seconds):
     }
 
 
-def cpu_baseline_mt(buf, n, pattern, seconds):
+def node_threads(world):
+    """Host threads for a node-wide CPU comparator: the process's CPU share,
+    at most 16 per GPU of the job (the GPU box grants 16 CPUs per GPU)."""
+    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(16 * max(1, world), cpus))
+
+
+def cpu_baseline_workers(buf, n, pattern, seconds, workers):
+    """The reference at N GPUs' worth of work: its coordinator hands one file to
+    each of N workers, and each worker's Map runs on ONE core
+    (map_reduce/worker.go:126-145; coordinator.go:312,329-333), re-compiling the
+    pattern per line (grep.go:21). Restated with the oracle: N threads, each
+    scanning its own part of the split (successive whole-line pieces from
+    offset i*n/N) with per-line compile, until `seconds` of wall time; value =
+    all threads' bytes / wall time (ctypes releases the GIL in the oracle)."""
+    import threading
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    done = [0] * workers
+    matches = [0] * workers
+    t0 = time.perf_counter()
+
+    def work(i):
+        pos = (n * i // workers)
+        end = n * (i + 1) // workers
+        host = buf[pos:min(end, pos + (64 << 20))].cpu().numpy().tobytes()  # this worker's part (<= 64 MiB)
+        a = host.find(b"\n") + 1 if i else 0  # start at a line start
+        piece = 64 << 10
+        while time.perf_counter() - t0 < seconds and a < len(host):
+            data = host[a:a + piece]
+            j = data.rfind(b"\n")
+            data = data[: j + 1] if j >= 0 else data
+            ln, _, _ = O.grep_map(pattern.encode(), data, recompile_per_line=True)
+            done[i] += len(data)
+            matches[i] += len(ln)
+            a += len(data)
+            piece = min(piece * 2, 1 << 20)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(workers)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(sum(done) / dt / 1e9, 6),
+        "unit": "GB/s",
+        "cores": workers,
+        "workers": workers,
+        "kind": "port",
+        "sample": "%d worker threads (the reference's N workers, one file each on one core), each on its own part of "
+                  "rank 0's split: %.2f MiB in all (%d matching lines), oracle/ grep.go Map restatement with "
+                  "per-line pattern compile (as grep.go:21), %.1f s wall" % (workers, sum(done) / 2**20,
+                                                                            sum(matches), dt),
+    }
+
+
+def cpu_baseline_mt(buf, n, pattern, seconds, threads=None):
     """SURVEY.md §8d comparator (3): the oracle's Map with the pattern compiled
-    once per call, lines split over T host threads (T = the box's CPU share,
-    at most 16). Bounded like cpu_baseline: doubling whole-line pieces from the
-    split's start (256 KiB up to 64 MiB, sized to the time left) until `seconds` of wall time are spent."""
+    once per call, lines split over T host threads (default T = the box's CPU
+    share, at most 16; at N > 1 the node's share, node_threads). Bounded like
+    cpu_baseline: doubling whole-line pieces from the split's start (256 KiB up
+    to 64 MiB, sized to the time left) until `seconds` of wall time are spent."""
     import ctypes
 
     import numpy as np
@@ -513,7 +681,7 @@ def cpu_baseline_mt(buf, n, pattern, seconds):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
-    T = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)))
+    T = threads or max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)))
     L = O.lib()
     pat = pattern.encode()
     piece, done, matches, dt = 256 << 10, 0, 0, 0.0
@@ -524,7 +692,7 @@ def cpu_baseline_mt(buf, n, pattern, seconds):
         cap = int(nl.size) + 1
         ln = np.zeros(cap, np.uint64)
         st = np.zeros(cap, np.uint64)
-        le = np.zeros(cap, np.uint32)
+        le = np.zeros(cap, np.uint64)
         t = time.perf_counter()
         cnt = L.orc_map_mt(pat, len(pat), data.ctypes.data, len(data), T, ln.ctypes.data, st.ctypes.data,
                            le.ctypes.data, cap)

@@ -41,7 +41,7 @@ struct OverflowLane {
   uint64_t cs;         // chunk start
   uint64_t out_base;   // its first staging index
   uint32_t nl_prefix;  // '\n' between the tile start and cs
-  uint32_t pad;
+  uint32_t pend;       // the lane's parked last line: pending index + 1 (0: none)
 };
 
 // A long line the scan parked (see park_pending): its start, the chunk boundary
@@ -66,6 +66,14 @@ struct ChunkMap {
   uint32_t pad;
 };
 constexpr uint32_t kNoNewline = 0xffffffffu;
+// LAZY record: the chunk's first '\n' lies in its first kLazyMapBytes, where
+// the scan computes no map (nearly every chunk of text): the resolution runs
+// the DFA over those bytes itself, from the state the earlier maps give.
+constexpr uint32_t kLazyNewline = 0xfffffffeu;
+#ifndef DGREP_LAZY_MAP_BYTES
+#define DGREP_LAZY_MAP_BYTES 0
+#endif
+constexpr uint32_t kLazyMapBytes = DGREP_LAZY_MAP_BYTES;  // a multiple of the Sheng block (0: maps from byte 0)
 
 // a segment of a parked line's remaining bytes (long_map_kernel)
 struct LongSeg {
@@ -134,10 +142,12 @@ struct LongArgs {
   const uint64_t* seg_off;  // [npend + 1]: line i's segments
   uint8_t* segmap;          // [nseg][256]
   // Sheng stepper (long_sheng_kernel): the scan's chunk maps, stepper state
-  // ids, start_m as a stepper id and V['\n'] (the 8 next states of '\n')
+  // ids, start_m as a stepper id and V['\n'] (the 8 next states of '\n');
+  // the whole V table (LAZY records are finished byte by byte)
   const ChunkMap* chunk_map;
   uint32_t sheng_m;
   uint32_t nl_lo, nl_hi;
+  const uint2* sheng_v;
 };
 
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids

@@ -24,7 +24,8 @@
 //     long_map_kernel, long_fin_kernel) then find its end from the per-chunk
 //     '\n' counts and run the DFA over it in parallel -- per-piece transition
 //     maps, composed in order -- instead of one lane reading on alone.
-//   * Per 4-byte word: 4 DFA steps by one of two steppers (below), newline
+//   * Per 4-byte word: 4 DFA steps by one of the steppers (StepSheng8,
+//     StepPair, StepTable, StepFilter, StepWide: see each struct), newline
 //     bookkeeping by SWAR on the word, and a matching line is detected by
 //     "state == START_M" (rare path).
 //       StepSheng8 (DFA <= 8 states): LDS holds, per input byte b, the 8-byte
@@ -35,12 +36,15 @@
 //       StepTable (DFA <= 256 states): u8 table [state][byte] with 260-byte
 //         rows (bank-staggered); a step is v_perm (row|byte) + v_lshl_add +
 //         ds_read_u8 on the dependent chain.
+//       StepPair: one two-byte table lookup per two bytes; StepFilter: the
+//         shallow states of a large DFA, lines leaving them verified after.
 //   * Matching lines are parked in per-lane LDS slots, counted, then the tile's
 //     lines are appended to a staging buffer with ONE atomic per tile, in
 //     ascending order inside the tile (no workgroup barrier anywhere: waves
-//     are independent). Three small passes (tile_reduce / block_scan /
-//     order_lines) turn tile-relative line numbers into global ones and lay
-//     the tiles out in split order.
+//     are independent). Two small passes (tile_scan_kernel: one workgroup's
+//     exclusive scan of the per-tile counts; order_lines_kernel: a wave per
+//     tile) turn tile-relative line numbers into global ones and lay the
+//     tiles out in split order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -476,6 +480,7 @@ struct LaneRun {
   int64_t prev_nl;   // position of the last consumed '\n' (-1: none / split start)
   bool seen;         // a line boundary has been crossed (owned lines begin)
   bool term;         // the terminating '\n' at or after the chunk end was consumed
+  bool parked;       // the last owned line was parked (park_pending) in this tile
   uint32_t nev;      // matching lines emitted
 };
 // ScanArgs::tails entry of a lane whose last record's slot holds kSlotLong: the
@@ -497,6 +502,12 @@ struct Emitter {
   // only the map-mode blocks hold it)
   uint4* cmap = nullptr;
   uint2* mapsl = nullptr;
+  // direct mode (overflow pass): the lane this sub-lane re-runs parked its last
+  // line at chunk-relative `park_at` (0: it did not) as pending entry park_idx;
+  // the sub-lane that reaches that point stages the same PENDING record instead
+  // of reading the long line on alone
+  uint64_t park_at = 0;
+  uint32_t park_idx = 0;
 
   // cand: a filter candidate (verified afterwards)
   __device__ __forceinline__ void operator()(LaneRun& r, uint64_t q, int64_t start, uint32_t rel,
@@ -545,9 +556,21 @@ struct Emitter {
     }
     ++r.nev;
   }
+  // direct mode: the PENDING record of the line parked at park_at (see above)
+  __device__ __forceinline__ void pending_direct(LaneRun& r, int64_t start, uint32_t rel) const {
+    const uint64_t o = out_base + r.nev;
+    if (o < a->capacity) {
+      StagedLine L;
+      L.start = cs + uint64_t(start);
+      L.len_lo = park_idx;
+      L.meta = (nl_prefix + rel) | kMetaPend;
+      a->staging[o] = L;
+    }
+    ++r.nev;
+  }
   // The same for a line wholly inside the lane's chunk (start < q < C <= 32 KiB):
   // 32-bit chunk-relative positions, no length checks.
-  // inner() for the slot mode with a dummy slot E (DGREP_FLAT_EMIT): own = the
+  // inner() for the slot mode with a dummy slot E (flat_emit()): own = the
   // lane owns the line. A write for a line it does not own lands in a slot (or
   // spill entry) no record has claimed yet, so it is never read.
   __device__ __forceinline__ void inner_flat(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand,
@@ -611,6 +634,20 @@ __device__ __forceinline__ uint32_t lnl_update(uint32_t lnl, uint32_t m) {
 }
 // block offset of the '\n' that lnl (>= kLnlBase) records
 __device__ __forceinline__ uint32_t lnl_pos(uint32_t lnl) { return (lnl >> 3) - (3u + kLnlOff); }
+
+// Steppers whose blocks start lnl from the lane's previous '\n' (the sentinel
+// start above); the others start every block at 0 and take the line start
+// from r.prev_nl with a select. Bit k = stepper kind k. Same-box A/B: the
+// sentinel wins on the pair stepper (C3 kernel 4,116 -> 4,282 GB/s), whose
+// event path runs in ~27 % of words, and costs the Sheng stepper 1.8 % (C2,
+// profiles/r03/ablation/sentinel_c2.txt): a per-block init for a rare path.
+#ifndef DGREP_SENTINEL_KINDS
+#define DGREP_SENTINEL_KINDS ((1 << kStepPair) | (1 << kStepFilter) | (1 << kStepTable) | (1 << kStepWide))
+#endif
+template <class Step>
+constexpr bool sentinel() {
+  return ((DGREP_SENTINEL_KINDS) >> Step::kKind) & 1;
+}
 
 // the steppers whose lanes carry the dummy slot (slot_stride): one stream per lane
 template <class Step, bool DIRECT>
@@ -716,19 +753,27 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
   if (!b.past && (m & (m - 1u)) == 0u) {
     // branch-free operands (selects, no nested exec-mask regions)
     const uint32_t k = uint32_t(__builtin_ctz(m)) >> 3;
-    // the line starts one byte after the '\n' lnl records (inside the chunk,
-    // lnl also encodes r.prev_nl: see lnl_update)
-    const uint32_t start = uint32_t(b.pos) + (b.lnl >> 3) - (2u + kLnlOff);
+    // the line starts one byte after the '\n' lnl records (sentinel steppers:
+    // inside the chunk lnl also encodes r.prev_nl, see lnl_update)
+    uint32_t start;
+    bool own;
+    if constexpr (sentinel<Step>()) {
+      start = uint32_t(b.pos) + (b.lnl >> 3) - (2u + kLnlOff);
+      own = b.lnl != 0;
+    } else {
+      start = b.lnl ? uint32_t(b.pos) + (b.lnl >> 3) - (2u + kLnlOff) : uint32_t(r.prev_nl) + 1u;
+      own = r.seen | (b.lnl != 0);
+    }
     const uint32_t sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
     if constexpr (flat_emit<Step, DIRECT>())
-      emit.inner_flat(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, cand_of(st, sk), b.lnl != 0);
-    else if (b.lnl != 0)
+      emit.inner_flat(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, cand_of(st, sk), own);
+    else if (own)
       emit.inner(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, cand_of(st, sk));
     return;
   }
   const uint64_t q0 = b.pos + 4u * J;
   const bool nl_w = b.lnl >= kLnlBase;  // a '\n' in an earlier word of this block
-  const bool seen_w = b.lnl != 0;
+  const bool seen_w = sentinel<Step>() ? b.lnl != 0 : (r.seen || b.lnl != 0);
   const bool term_w = r.term || (b.past && nl_w);
   const int64_t prev_w = nl_w ? int64_t(b.pos + lnl_pos(b.lnl)) : r.prev_nl;
   uint32_t evm;
@@ -765,12 +810,16 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
   word_nl<J>(m, b);
 }
 
+template <bool SENT>
 __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const LaneRun& r) {
   b.pos = pos;
   b.past = pos >= C;
   b.nlrun = r.nl;
   // inside the chunk: r.prev_nl - pos >= -(C + 1) > -kLnlOff
-  b.lnl = !r.seen ? 0u : b.past ? kLnlSeen : 8u * uint32_t(int32_t(r.prev_nl - int64_t(pos)) + int32_t(3u + kLnlOff));
+  if constexpr (SENT)
+    b.lnl = !r.seen ? 0u : b.past ? kLnlSeen : 8u * uint32_t(int32_t(r.prev_nl - int64_t(pos)) + int32_t(3u + kLnlOff));
+  else
+    b.lnl = 0u;
 }
 
 __device__ __forceinline__ void blk_finish(const Blk& b, uint32_t s, LaneRun& r) {
@@ -789,8 +838,8 @@ __device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uin
                                            const uint4 (&vb)[BK / 16], uint64_t pos, uint64_t C, LaneRun& ra,
                                            LaneRun& rb, const Emitter<E, DIRECT>& ea, const Emitter<E, DIRECT>& eb) {
   Blk ba, bb;
-  blk_init(ba, pos, C, ra);
-  blk_init(bb, pos, C, rb);
+  blk_init<sentinel<Step>()>(ba, pos, C, ra);
+  blk_init<sentinel<Step>()>(bb, pos, C, rb);
   uint32_t sa = ra.s, sb = rb.s;
   constexpr int NW = BK / 4;
   uint32_t wa[NW], wb[NW];
@@ -828,7 +877,7 @@ template <int BK, bool MAP, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
-  blk_init(b, pos, C, r);
+  blk_init<sentinel<Step>()>(b, pos, C, r);
   uint32_t s = r.s;
   // word j's state-independent work (Step::prep) is issued one word ahead
   constexpr int NW = BK / 4;
@@ -887,6 +936,19 @@ __device__ __forceinline__ void run_tail(const Step& st, uint32_t M, const uint8
     mlo = v.x;
     mhi = v.y;
   }
+  if constexpr (Step::kKind == kStepSheng8 && kLazyMapBytes != 0) {
+    // the split ends before the lazy point (run_lane_from never reached it):
+    // a '\n' already seen makes a LAZY record; else the map starts at byte 0
+    if (emit.cmap && pos < kLazyMapBytes) {
+      if (r.nl != 0u) {
+        *emit.cmap = make_uint4(0u, 0u, kLazyNewline, 0u);
+      } else {
+        mlo = 0x03020100u;
+        mhi = 0x07060504u;
+        for (uint64_t q = 0; q < pos; ++q) st.compose_byte(p[q], mlo, mhi);
+      }
+    }
+  }
   for (; pos < avail; ++pos) {
     if (pos == C) {
       nl_chunk = r.nl;
@@ -924,6 +986,7 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
   r.prev_nl = -1;
   r.seen = (cs == 0);
   r.term = false;
+  r.parked = false;
   r.nev = 0;
 }
 
@@ -977,6 +1040,26 @@ __device__ __forceinline__ void park_pending(const ScanArgs& a, uint64_t cs, uin
   }
   emit.pending(r, r.prev_nl + 1, r.nl, idx);
   r.term = true;
+  r.parked = true;
+}
+
+// Sheng chunk maps, lazily: a lane that reaches kLazyMapBytes without a '\n'
+// composes the map of those bytes now (read again, from L2) and goes on in
+// map mode; in text nearly every lane has met a '\n' by then, so the wave
+// skips map mode entirely (same-box A/B, C2: map-mode blocks from byte 0 cost
+// 0.8 %, profiles/r04/ablation).
+template <class Step>
+__device__ __forceinline__ void lazy_map(const Step& st, const uint8_t* p, uint2* mapsl) {
+  uint32_t lo = 0x03020100u, hi = 0x07060504u;
+#pragma unroll 1
+  for (uint32_t q = 0; q < kLazyMapBytes; q += 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p + q);
+    st.compose(st.prep(v.x), 3, lo, hi);
+    st.compose(st.prep(v.y), 3, lo, hi);
+    st.compose(st.prep(v.z), 3, lo, hi);
+    st.compose(st.prep(v.w), 3, lo, hi);
+  }
+  *mapsl = make_uint2(lo, hi);
 }
 
 // Runs a lane (see file comment) from chunk-relative position pos0 over
@@ -1010,11 +1093,17 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   if (maps && pos0 == 0) *emit.mapsl = make_uint2(0x03020100u, 0x07060504u);  // identity
   if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
 #define DG_STEP(V)                                                                         \
-  if (kMap && __ballot(maps && r.nl == 0u && pos < uint64_t(C)) != 0)                      \
+  if (kMap && __ballot(maps && r.nl == 0u && pos >= kLazyMapBytes && pos < uint64_t(C)) != 0) \
     run_block<BK, kMap>(st, M, V, pos, uint64_t(C), r, emit);                              \
   else                                                                                     \
     run_block<BK, false>(st, M, V, pos, uint64_t(C), r, emit);
 #define DG_CHECK                                                                           \
+  if (kMap && kLazyMapBytes != 0 && maps && pos == kLazyMapBytes) {                        \
+    if (r.nl != 0u)                                                                        \
+      *emit.cmap = make_uint4(0u, 0u, kLazyNewline, 0u); /* resolved from the bytes */    \
+    else                                                                                   \
+      lazy_map(st, p, emit.mapsl);                                                         \
+  }                                                                                        \
   if (pos == uint64_t(C)) {                                                                \
     nl_chunk = r.nl;                                                                       \
     snap = true;                                                                           \
@@ -1027,6 +1116,14 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
     }                                                                                      \
   }                                                                                        \
   if (lane_done(pos, uint64_t(C), r)) break;                                               \
+  if constexpr (DIRECT) {                                                                  \
+    if (emit.park_at && pos == emit.park_at) {                                             \
+      /* the main scan parked this line here: the same pending entry decides it */         \
+      emit.pending_direct(r, r.prev_nl + 1, r.nl);                                         \
+      r.term = true;                                                                       \
+      break;                                                                               \
+    }                                                                                      \
+  }                                                                                        \
   if constexpr (kTrack) {                                                                  \
     if (maps && pos == uint64_t(C) + kParkAfter) {                                         \
       /* parked at C: the chunk maps from C on finish it */                                \
@@ -1293,7 +1390,8 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
           ol.cs = cs[k];
           ol.out_base = o0;
           ol.nl_prefix = nl_off[k];
-          ol.pad = 0;
+          // a parked last line: its pending index + 1 (the pass stops there too)
+          ol.pend = r[k].parked ? uint32_t(tails[k] & ~kTailPending) + 1u : 0u;
           a.overflow[q] = ol;
         }
       }
@@ -1331,11 +1429,16 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
     const bool live = lane < nsub;
     const uint64_t cs = ol.cs + uint64_t(lane) * sc;
     const uint32_t len = live ? min(sc, C - lane * sc) : 0u;
+    // where the main scan parked the lane's last line (park_pending): C +
+    // kParkAfter with Sheng chunk maps, else 2 C -- relative to this sub-lane
+    const uint64_t park = uint64_t(C) + (Step::kKind == kStepSheng8 && a.chunk_map ? kParkAfter : uint64_t(C));
+    const uint64_t park_at = ol.pend ? park - uint64_t(lane) * sc : 0;
     LaneRun r;
     uint32_t nl = 0, nev = 0;
     if (live) {
       // out_base = capacity: every write of the counting pass is skipped
       Emitter<E, true> cnt{&a, nullptr, cs, a.capacity, 0};
+      cnt.park_at = park_at;
       nl = run_lane<BK>(a, st, cs, r, cnt, len);
       nev = r.nev;
     }
@@ -1343,6 +1446,8 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
     const uint32_t ev_off = wave_incl_scan(nev) - nev;
     if (live && nev) {
       Emitter<E, true> ed{&a, nullptr, cs, ol.out_base + ev_off, ol.nl_prefix + nl_off};
+      ed.park_at = park_at;
+      ed.park_idx = ol.pend - 1u;
       run_lane<BK>(a, st, cs, r, ed, len);
     }
   }
@@ -1731,12 +1836,14 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
   __shared__ uint2 wmap[kLsThreads / 64];
   __shared__ uint32_t whit[kLsThreads / 64];
   __shared__ uint64_t wend[kLsThreads / 64];
+  __shared__ uint32_t wlazy[kLsThreads / 64];
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint2 ident = make_uint2(0x03020100u, 0x07060504u);
   for (uint64_t i = blockIdx.x; i < la.npend; i += gridDim.x) {
     const PendingLine P = la.pend[i];
     uint32_t s = P.state;
     uint64_t end = la.n;
+    bool lazy = false;  // the stopping chunk is a LAZY record: `end` is its start
     for (uint64_t c0 = P.resume / la.chunk;; c0 += uint64_t(kLsThreads) * kLsPer) {
       // this thread's chunks, in order, up to the first that holds a '\n' (or
       // lies past the split)
@@ -1749,7 +1856,7 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
         cm[j] = ChunkMap{v.x, v.y, v.z, v.w};
       }
       uint2 m = ident;
-      bool stop = false;
+      bool stop = false, lz = false;
       uint64_t e = 0;
 #pragma unroll
       for (int j = 0; j < kLsPer; ++j) {
@@ -1757,6 +1864,9 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
         if (cm[j].pad) {  // past the split's end
           stop = true;
           e = la.n;
+        } else if (cm[j].first == kLazyNewline) {  // no map: stop before this chunk
+          stop = lz = true;
+          e = (cb + j) * la.chunk;
         } else {
           m = map_then(m, make_uint2(cm[j].lo, cm[j].hi));
           if (cm[j].first != kNoNewline) {
@@ -1778,7 +1888,10 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
         wmap[w] = m;
         whit[w] = hl;
       }
-      if (lane == hl) wend[w] = e;
+      if (lane == hl) {
+        wend[w] = e;
+        wlazy[w] = lz ? 1u : 0u;
+      }
       __syncthreads();
       uint32_t wf = kLsThreads / 64;
       for (uint32_t k = 0; k < kLsThreads / 64; ++k) {
@@ -1788,13 +1901,29 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
           if (whit[k] < 64u) wf = k;
         }
       }
-      if (wf < kLsThreads / 64) end = wend[wf];
+      if (wf < kLsThreads / 64) {
+        end = wend[wf];
+        lazy = wlazy[wf] != 0u;
+      }
       __syncthreads();  // wmap / whit / wend are rewritten by the next round
       if (wf < kLsThreads / 64) break;
     }
+    // a LAZY chunk: its first '\n' lies in its first kLazyMapBytes; s is the
+    // state at the chunk's start, so step its bytes through that '\n'
+    if (lazy && threadIdx.x == 0) {
+      for (uint64_t q = end;; ++q) {
+        const uint32_t b = la.data[q];
+        const uint2 v = la.sheng_v[b];
+        s = __builtin_amdgcn_perm(v.y, v.x, s) & 0xffu;
+        if (b == uint32_t('\n')) {
+          end = q;
+          break;
+        }
+      }
+    }
     // end < n: the last map ended with the line's '\n'; end == n: the split
     // ended first, and its end closes the line (V['\n'] applied)
-    if (end == la.n) s = __builtin_amdgcn_perm(la.nl_hi, la.nl_lo, s) & 0xffu;
+    if (!lazy && end == la.n) s = __builtin_amdgcn_perm(la.nl_hi, la.nl_lo, s) & 0xffu;
     if (threadIdx.x == 0) {
       PendingLine Q = P;
       Q.end = end;

@@ -39,6 +39,15 @@
 #ifndef DGREP_SPILL_RECORDS
 #define DGREP_SPILL_RECORDS 240
 #endif
+// A/B knobs (shipped: 1, 1): park long lines at all (0: a lane reads its last
+// line to its end), and the Sheng stepper's chunk maps (0: Sheng parks at 2 C
+// and resolves through the per-chunk '\n' counts like the other steppers)
+#ifndef DGREP_PARK
+#define DGREP_PARK 1
+#endif
+#ifndef DGREP_SHENG_MAPS
+#define DGREP_SHENG_MAPS 1
+#endif
 
 namespace dgrep {
 // scan_dfa.hip
@@ -418,6 +427,12 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
 
 extern "C" const char* dgrep_last_error(dgrep_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+// for exchange.hip (the communicator runs on its context's device and stream)
+namespace dgrep {
+int ctx_device(const dgrep_ctx* c) { return c->device; }
+hipStream_t ctx_stream(const dgrep_ctx* c) { return c->stream; }
+}  // namespace dgrep
+
 extern "C" int dgrep_set_stream(dgrep_ctx* c, void* s) {
   if (!c) return DGREP_E_INVALID;
   c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
@@ -774,10 +789,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   // table steppers)
   const uint32_t streams = tile / (uint64_t(kTileLanes) * chunk);
   if ((rc = grow(c, &c->d_tails, &c->tails_cap, uint64_t(grid) * threads * streams)) != DGREP_OK) return rc;
-  const bool park = c->d_long_tbl != nullptr;
+  const bool park = DGREP_PARK && c->d_long_tbl != nullptr;
   const uint64_t nchunks = (n + chunk - 1) / chunk;
   // Sheng: the chunk maps replace the '\n' counts (long_sheng_kernel)
-  const bool park_maps = park && c->step_kind == kStepSheng8;
+  const bool park_maps = park && c->step_kind == kStepSheng8 && DGREP_SHENG_MAPS;
   if (park) {
     if (park_maps) {
       if ((rc = grow(c, &c->d_chunk_map, &c->chunk_map_cap, nchunks)) != DGREP_OK) return rc;
@@ -910,6 +925,8 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
       la.sheng_m = c->start_m;
       la.nl_lo = c->sheng_nl_lo;
       la.nl_hi = c->sheng_nl_hi;
+      la.sheng_v = reinterpret_cast<const uint2*>(c->d_table);
+      la.data = d_data;
       HIPCHK(long_lines_sheng(la, c->stream));
     } else if (npend && (rc = resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) {
       return rc;
@@ -923,6 +940,40 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     c->last_ms += S.verify_ms;
     total = staged - removed;
     S.candidates = removed;  // dropped ones; kept candidates count as matches
+  } else if (npend && staged > a.capacity) {
+    // The staged lines did not fit (a size query, or too small a capacity), so
+    // no record is resolved -- but the count must still be exact: every parked
+    // line was counted as one staged record, so resolve the pending list (it
+    // does not depend on staging) and subtract the parked lines that do not
+    // match. (Overflow lanes were counted in full by the scan: no pass needed.)
+    HIPCHK(hipEventRecord(c->ev4, c->stream));
+    if (park_maps) {
+      LongArgs la;
+      memset(&la, 0, sizeof la);
+      la.n = n;
+      la.chunk = chunk;
+      la.nchunks = nchunks;
+      la.pend = c->d_pend;
+      la.npend = npend;
+      la.chunk_map = c->d_chunk_map;
+      la.sheng_m = c->start_m;
+      la.nl_lo = c->sheng_nl_lo;
+      la.nl_hi = c->sheng_nl_hi;
+      la.sheng_v = reinterpret_cast<const uint2*>(c->d_table);
+      la.data = d_data;
+      HIPCHK(long_lines_sheng(la, c->stream));
+    } else if ((rc = resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) {
+      return rc;
+    }
+    HIPCHK(hipEventRecord(c->ev5, c->stream));
+    std::vector<PendingLine> P(npend);
+    HIPCHK(hipMemcpyAsync(P.data(), c->d_pend, npend * sizeof(PendingLine), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventElapsedTime(&S.verify_ms, c->ev4, c->ev5));
+    c->last_ms += S.verify_ms;
+    uint64_t unmatched = 0;
+    for (const PendingLine& p : P) unmatched += p.matched ? 0u : 1u;
+    total = staged - unmatched;
   }
   if (filt) c->staged_hint = staged;
   S.matches = total;

@@ -55,7 +55,10 @@ EXPORTS = (
     "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_lane_chunk", "dgrep_set_ingest", "dgrep_last_ingest_ms",
     "dgrep_map_partitions", "dgrep_partitions_free", "dgrep_encode_device", "dgrep_last_encode_ms",
     "dgrep_reduce", "dgrep_reduce_free", "dgrep_last_scan_stats", "dgrep_build_info",
+    "dgrep_comm_unique_id", "dgrep_comm_open", "dgrep_comm_close", "dgrep_gather_records_device",
+    "dgrep_gather_records", "dgrep_gathered_free", "dgrep_comm_last_error",
 )
+COMM_ID_BYTES = 128
 
 STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair", 4: "filter"}
 
@@ -91,6 +94,12 @@ class _ScanStats(ctypes.Structure):
                 ("scan_attempts", ctypes.c_uint32), ("tiles", ctypes.c_uint64), ("overflow_lanes", ctypes.c_uint64),
                 ("matches", ctypes.c_uint64), ("scan_ms", ctypes.c_float), ("overflow_ms", ctypes.c_float),
                 ("verify_ms", ctypes.c_float), ("candidates", ctypes.c_uint64), ("pending", ctypes.c_uint64)]
+
+
+class _Gathered(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64), ("line_no", ctypes.POINTER(ctypes.c_uint64)),
+                ("start", ctypes.POINTER(ctypes.c_uint64)), ("len", ctypes.POINTER(ctypes.c_uint64)),
+                ("split", ctypes.POINTER(ctypes.c_uint32))]
 
 
 class _BlobInfo(ctypes.Structure):
@@ -172,6 +181,21 @@ def lib() -> ctypes.CDLL:
             L.dgrep_last_scan_stats.restype = i
             L.dgrep_build_info.argtypes = []
             L.dgrep_build_info.restype = ctypes.c_char_p
+            L.dgrep_comm_unique_id.argtypes = [vp]
+            L.dgrep_comm_unique_id.restype = i
+            L.dgrep_comm_open.argtypes = [vp, vp, i, i, ctypes.POINTER(vp)]
+            L.dgrep_comm_open.restype = i
+            L.dgrep_comm_close.argtypes = [vp]
+            L.dgrep_comm_close.restype = None
+            L.dgrep_gather_records_device.argtypes = [vp, vp, vp, vp, u64, ctypes.c_uint32, i, ctypes.POINTER(vp),
+                                                      ctypes.POINTER(u64), vp]
+            L.dgrep_gather_records_device.restype = i
+            L.dgrep_gather_records.argtypes = [vp, vp, vp, vp, u64, ctypes.c_uint32, i, ctypes.POINTER(_Gathered)]
+            L.dgrep_gather_records.restype = i
+            L.dgrep_gathered_free.argtypes = [ctypes.POINTER(_Gathered)]
+            L.dgrep_gathered_free.restype = None
+            L.dgrep_comm_last_error.argtypes = [vp]
+            L.dgrep_comm_last_error.restype = ctypes.c_char_p
             _lib = L
     return _lib
 
@@ -418,6 +442,80 @@ def synth_keywords(seed: int, count: int = 1000) -> List[bytes]:
 
 pattern: str = os.environ.get("DGREP_PATTERN", "")  # grep.go:11 `var pattern string = ""`
 
+class Comm:
+    """The C ABI's multi-GPU exchange (include/dgrep.h, dgrep_comm_*): an RCCL
+    communicator on a Context's device and stream. Rank 0 (or any one rank)
+    makes the id with :meth:`unique_id` and hands the 128 bytes to the others;
+    every rank then constructs a Comm (collective)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        rc = lib().dgrep_comm_unique_id(buf)
+        if rc != DGREP_OK:
+            raise DgrepError(rc, "dgrep_comm_unique_id failed")
+        return buf.raw
+
+    def __init__(self, ctx: "Context", uid: bytes, nranks: int, rank: int):
+        self._L = lib()
+        self.ctx, self.nranks, self.rank = ctx, nranks, rank
+        h = ctypes.c_void_p()
+        rc = self._L.dgrep_comm_open(ctx._h, ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES), nranks, rank,
+                                     ctypes.byref(h))
+        self._h = h
+        if rc != DGREP_OK:
+            msg = self._err()
+            self.close()
+            raise DgrepError(rc, msg)
+
+    def _err(self) -> str:
+        m = self._L.dgrep_comm_last_error(self._h) if self._h else None
+        return m.decode(errors="replace") if m else ""
+
+    def gather_device(self, d_line: int, d_start: int, d_len: int, count: int, split: int = 0, root: int = 0):
+        """dgrep_gather_records_device: (device pointer of the packed 28-B
+        records, total, per-rank counts) on the root; (None, count, None) elsewhere."""
+        ptr = ctypes.c_void_p()
+        total = ctypes.c_uint64()
+        counts = (ctypes.c_uint64 * self.nranks)()
+        rc = self._L.dgrep_gather_records_device(self._h, d_line, d_start, d_len, count, split & 0xFFFFFFFF, root,
+                                                 ctypes.byref(ptr), ctypes.byref(total), counts)
+        if rc != DGREP_OK:
+            raise DgrepError(rc, self._err())
+        if self.rank != root:
+            return None, total.value, None
+        return ptr.value, total.value, list(counts)
+
+    def gather(self, d_line: int, d_start: int, d_len: int, count: int, split: int = 0, root: int = 0):
+        """dgrep_gather_records: (line_no, start, len, split) numpy arrays on the
+        root (rank order), None elsewhere."""
+        g = _Gathered()
+        rc = self._L.dgrep_gather_records(self._h, d_line, d_start, d_len, count, split & 0xFFFFFFFF, root,
+                                          ctypes.byref(g))
+        if rc != DGREP_OK:
+            raise DgrepError(rc, self._err())
+        try:
+            if self.rank != root:
+                return None
+            n = g.count
+            arr = lambda p, t: np.ctypeslib.as_array(p, shape=(n,)).astype(t) if n else np.zeros(0, t)
+            return (arr(g.line_no, np.uint64), arr(g.start, np.uint64), arr(g.len, np.uint64),
+                    arr(g.split, np.uint32))
+        finally:
+            self._L.dgrep_gathered_free(ctypes.byref(g))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.dgrep_comm_close(self._h)
+        self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 _ctx_local = threading.local()
 
 
@@ -436,10 +534,20 @@ def pick_device(worker_id: int = -1) -> int:
     return d.value
 
 
+def _default_device() -> int:
+    """The module-level Map's device: the worker rule (pick_device) only when
+    DGREP_DEVICE or DGREP_WORKER_ID says which worker this is; otherwise device
+    0, as before round 3 (never a device that depends on the process id, which
+    could differ from the caller's torch device)."""
+    if os.environ.get("DGREP_DEVICE") or os.environ.get("DGREP_WORKER_ID"):
+        return pick_device()
+    return 0
+
+
 def _context() -> Context:
     ctx = getattr(_ctx_local, "ctx", None)
     if ctx is None:
-        ctx = Context(pick_device())
+        ctx = Context(_default_device())
         _ctx_local.ctx = ctx
         _ctx_local.loaded = None
     if _ctx_local.loaded != pattern:

@@ -203,6 +203,49 @@ void dgrep_reduce_free(dgrep_reduce_out* r);
 int dgrep_scan_device(dgrep_ctx* ctx, const void* d_data, size_t n, uint64_t* d_line_no, uint64_t* d_start,
                       uint64_t* d_len, uint64_t capacity, uint64_t* count);
 
+/* ---- multi-GPU exchange -----------------------------------
+ * Replaces the SFTP shipping of map output to the reducers
+ * (map_reduce/coordinator.go:136-142) for workers on one node: each worker
+ * process scans its split on its own GPU and the compacted match records --
+ * never the line bytes -- are gathered to the reducing worker over RCCL
+ * (xGMI). Callable from the Go worker through cgo like the rest of the ABI.
+ * Setup: the root calls dgrep_comm_unique_id and hands the 128 bytes to the
+ * other workers out of band (the worker's own channel, e.g. a file or its RPC);
+ * every worker then calls dgrep_comm_open with its rank (collective: all
+ * nranks must call it). The communicator uses the context's device and stream. */
+#define DGREP_COMM_ID_BYTES 128
+typedef struct dgrep_comm dgrep_comm;
+int dgrep_comm_unique_id(void* id_out /* DGREP_COMM_ID_BYTES */);
+int dgrep_comm_open(dgrep_ctx* ctx, const void* id, int nranks, int rank, dgrep_comm** comm);
+void dgrep_comm_close(dgrep_comm* comm);
+/* Gather every rank's records (a dgrep_scan_device result: `count` entries of
+ * the three device arrays) to rank `root`, as 28-byte packed records
+ * {u64 line_no, u64 start, u64 len, u32 split} (split = the caller's map task
+ * id, so the root can rebuild each Key = Sprintf(filename[split], line_no),
+ * application/grep.go:25), in rank order. Collective. The counts are
+ * all-gathered first (8 B per rank), then one grouped send/recv moves exactly
+ * sum(counts) x 28 bytes into a device buffer the communicator owns (grown as
+ * needed): on the root *d_records points at it (valid until the next gather or
+ * dgrep_comm_close), *total = sum(counts), and rank_counts (may be NULL)
+ * receives the nranks counts. Other ranks: *d_records = NULL, *total = count. */
+int dgrep_gather_records_device(dgrep_comm* comm, const uint64_t* d_line_no, const uint64_t* d_start,
+                                const uint64_t* d_len, uint64_t count, uint32_t split, int root,
+                                const void** d_records, uint64_t* total, uint64_t* rank_counts);
+/* The same with host results on the root (SoA, malloc'd; free with
+ * dgrep_gathered_free); other ranks get count 0. */
+typedef struct {
+  uint64_t count;
+  uint64_t* line_no;
+  uint64_t* start;
+  uint64_t* len;
+  uint32_t* split;
+} dgrep_gathered;
+int dgrep_gather_records(dgrep_comm* comm, const uint64_t* d_line_no, const uint64_t* d_start, const uint64_t* d_len,
+                         uint64_t count, uint32_t split, int root, dgrep_gathered* out);
+void dgrep_gathered_free(dgrep_gathered* g);
+/* message for the communicator's last non-OK status (RCCL / HIP error text) */
+const char* dgrep_comm_last_error(dgrep_comm* comm);
+
 /* ---- bench / test tooling ------------------------------------------------ */
 /* Fill d_out[0:n) with the seeded synthetic log corpus on
  * the device. kind: 0 = plain log lines, 1 = log lines with seeded

@@ -19,7 +19,7 @@
  * one empty line). Each piece is matched on its own; the error returned by
  * regexp.Match is discarded (grep.go:21), so a bad pattern matches nothing. */
 int64_t orc_map(const char* pat, size_t patn, const unsigned char* contents, size_t n,
-                int recompile_per_line, uint64_t* line_no, uint64_t* start, uint32_t* len,
+                int recompile_per_line, uint64_t* line_no, uint64_t* start, uint64_t* len,
                 uint64_t cap) {
   orc_re* re = NULL;
   int st = orc_compile(pat, patn, &re, NULL, 0);
@@ -45,7 +45,7 @@ int64_t orc_map(const char* pat, size_t patn, const unsigned char* contents, siz
       if ((uint64_t)cnt < cap) {
         if (line_no) line_no[cnt] = ln;
         if (start) start[cnt] = ls;
-        if (len) len[cnt] = (uint32_t)(le - ls);
+        if (len) len[cnt] = (uint64_t)(le - ls);
       }
       cnt++;
     }
@@ -62,7 +62,7 @@ typedef struct {
   size_t lo, hi;        /* byte range of whole lines [lo, hi) */
   uint64_t first_line;  /* 1-based number of the line starting at lo */
   int last;             /* this slice owns the final (possibly empty) line */
-  uint64_t* ln; uint64_t* st; uint32_t* lens; uint64_t cnt, cap;
+  uint64_t* ln; uint64_t* st; uint64_t* lens; uint64_t cnt, cap;
 } Slice;
 
 static void* slice_run(void* arg) {
@@ -79,9 +79,9 @@ static void* slice_run(void* arg) {
         s->cap = s->cap ? s->cap * 2 : 1024;
         s->ln = realloc(s->ln, s->cap * sizeof(uint64_t));
         s->st = realloc(s->st, s->cap * sizeof(uint64_t));
-        s->lens = realloc(s->lens, s->cap * sizeof(uint32_t));
+        s->lens = realloc(s->lens, s->cap * sizeof(uint64_t));
       }
-      s->ln[s->cnt] = ln; s->st[s->cnt] = ls; s->lens[s->cnt] = (uint32_t)(le - ls);
+      s->ln[s->cnt] = ln; s->st[s->cnt] = ls; s->lens[s->cnt] = (uint64_t)(le - ls);
       s->cnt++;
     }
     ln++;
@@ -93,7 +93,7 @@ static void* slice_run(void* arg) {
 }
 
 int64_t orc_map_mt(const char* pat, size_t patn, const unsigned char* contents, size_t n,
-                   int nthreads, uint64_t* line_no, uint64_t* start, uint32_t* len, uint64_t cap) {
+                   int nthreads, uint64_t* line_no, uint64_t* start, uint64_t* len, uint64_t cap) {
   orc_re* re = NULL;
   int st = orc_compile(pat, patn, &re, NULL, 0);
   if (st == ORC_EUNSUPPORTED) { orc_free(re); return -1; }

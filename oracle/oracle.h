@@ -60,11 +60,11 @@ void orc_matcher_free(orc_matcher* m);
  * the pattern is unsupported by the restatement. A Go syntax error yields 0.
  */
 int64_t orc_map(const char* pat, size_t patn, const unsigned char* contents, size_t n,
-                int recompile_per_line, uint64_t* line_no, uint64_t* start, uint32_t* len,
+                int recompile_per_line, uint64_t* line_no, uint64_t* start, uint64_t* len,
                 uint64_t cap);
 /* Same as orc_map with one thread per slice of lines (pattern compiled once). */
 int64_t orc_map_mt(const char* pat, size_t patn, const unsigned char* contents, size_t n,
-                   int nthreads, uint64_t* line_no, uint64_t* start, uint32_t* len, uint64_t cap);
+                   int nthreads, uint64_t* line_no, uint64_t* start, uint64_t* len, uint64_t cap);
 
 /* map_reduce/worker.go:13-17: FNV-1a 32 & 0x7fffffff. */
 uint32_t orc_ihash(const unsigned char* key, size_t n);

@@ -78,7 +78,7 @@ def compile_status(pattern: bytes) -> int:
 
 
 def grep_map(pattern: bytes, contents: bytes, recompile_per_line=False, threads=0):
-    """grep.go Map restated: returns (line_no u64[], start u64[], len u32[])."""
+    """grep.go Map restated: returns (line_no u64[], start u64[], len u64[])."""
     if isinstance(pattern, str):
         pattern = pattern.encode()
     buf = np.frombuffer(contents, dtype=np.uint8) if len(contents) else np.zeros(1, np.uint8)
@@ -89,7 +89,7 @@ def grep_map(pattern: bytes, contents: bytes, recompile_per_line=False, threads=
     for _ in range(2):
         ln = np.zeros(max(cap, 1), np.uint64)
         st = np.zeros(max(cap, 1), np.uint64)
-        lens = np.zeros(max(cap, 1), np.uint32)
+        lens = np.zeros(max(cap, 1), np.uint64)
         if threads and threads > 1:
             cnt = L.orc_map_mt(pattern, len(pattern), ptr, len(contents), threads, ln.ctypes.data,
                                st.ctypes.data, lens.ctypes.data, cap)

@@ -33,7 +33,7 @@ def _unpack(v):
 
 
 def _want(v):
-    return (np.array(v["line_no"], np.uint64), np.array(v["start"], np.uint64), np.array(v["len"], np.uint32))
+    return (np.array(v["line_no"], np.uint64), np.array(v["start"], np.uint64), np.array(v["len"], np.uint64))
 
 
 def _eq(got, want, name):

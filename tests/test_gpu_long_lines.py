@@ -6,8 +6,7 @@ long-line kernels (end from the per-chunk '\\n' counts, per-segment transition
 maps composed in order) -- checked bit-exactly against the oracle for every
 such stepper, with matches at a line's start, middle and far end, lines ending
 exactly at chunk edges, newline-free and unterminated splits. A line over
-4 GiB is reported with its 64-bit length (structural check: the oracle's
-32-bit lengths cannot hold it)."""
+4 GiB is reported with its 64-bit length, checked against the oracle."""
 import random
 
 import numpy as np
@@ -109,8 +108,9 @@ def test_long_lines_workload_scale(gpu_ctx):
 def test_line_over_4gib(gpu_ctx):
     """One 4.5 GiB line (no '\\n') then a short one: the "" pattern (the
     reference's shipped grep.go:11) matches both; `error` planted 3 bytes
-    before the long line's end matches only it. Checked structurally: record
-    = whole line, 64-bit length, numbering."""
+    before the long line's end matches only it. Checked against the expected
+    records AND the oracle's Map over the same 4.5 GiB (64-bit lengths on
+    both sides since round 4)."""
     import torch
 
     n_long = (9 << 29) + 3  # 4.5 GiB + 3
@@ -119,6 +119,7 @@ def test_line_over_4gib(gpu_ctx):
     buf = torch.full((n + 64,), ord("x"), dtype=torch.uint8, device="cuda")
     buf[n_long - 8:n_long - 3] = torch.tensor(list(b"error"), dtype=torch.uint8, device="cuda")
     buf[n_long:n] = torch.tensor(list(tail), dtype=torch.uint8, device="cuda")
+    host = buf[:n].cpu().numpy()
     cap = 16
     line_t = torch.zeros(cap, dtype=torch.int64, device="cuda")
     start_t = torch.zeros(cap, dtype=torch.int64, device="cuda")
@@ -130,5 +131,75 @@ def test_line_over_4gib(gpu_ctx):
         got = list(zip(line_t[:cnt].tolist(), start_t[:cnt].tolist(), len_t[:cnt].tolist()))
         assert got == want, (pattern, got)
         assert gpu_ctx.scan_stats()["pending"] >= 1
-    del buf
+        oln, ost, ole = O.grep_map(pattern, host, threads=16)
+        assert list(zip(oln.tolist(), ost.tolist(), ole.tolist())) == want, pattern
+    del buf, host
     torch.cuda.empty_cache()
+
+
+def _dense_then_long(chunk, long_len, long_matches, dense=b"error", seed=3):
+    """Normal lines, then dense matching lines up to 64 bytes before a lane
+    chunk's end, then one line of long_len bytes (so the lane owning it also
+    owns hundreds of matching lines: it overflows AND parks), then normal lines."""
+    rnd = random.Random(seed)
+    head = b"".join(b"abc def %d\n" % rnd.randrange(1000) for _ in range(50))
+    target = ((len(head) // chunk) + 3) * chunk - 64  # the long line starts here
+    body = bytearray(head)
+    while len(body) + len(dense) + 1 <= target - 8:
+        body += dense + b"\n"
+    body += b"f" * (target - len(body) - 1) + b"\n"
+    assert len(body) == target
+    line = bytearray(b"q" * long_len)
+    if long_matches:
+        line[-5:] = b"error"
+    return bytes(body) + bytes(line) + b"\n" + b"tail line error\nlast\n"
+
+
+@pytest.mark.parametrize("force,pattern,chunk", [
+    ("auto", b"error", 4096),                      # Sheng (chunk maps: parked at C + 4 KiB)
+    ("auto", b"error", 32768),
+    ("auto", b"^[a-j ]*error[a-j ]*$", 4096),      # pair (parked at 2 C)
+    ("table", b"error$", 0),                       # u8 table, two 2 KiB chunks per lane
+])
+@pytest.mark.parametrize("long_matches", [False, True])
+def test_overflowing_lane_with_parked_line(gpu_ctx, force, pattern, chunk, long_matches):
+    """A lane that owns more matching lines than its slots + spill area AND
+    parks its last (long) line: the overflow pass re-runs it and must stop at
+    the same park point, staging the same pending record (a non-matching long
+    line left an unfilled record before round 4)."""
+    c = chunk or 2048
+    data = _dense_then_long(c, 6 * max(c, 4096) + 123, long_matches)
+    try:
+        gpu_ctx.set_stepper(force)
+        gpu_ctx.set_lane_chunk(chunk)
+        st = _check(gpu_ctx, pattern, data)
+        assert st["overflow_lanes"] > 0 and st["pending"] > 0, st
+    finally:
+        gpu_ctx.set_stepper("auto")
+        gpu_ctx.set_lane_chunk(0)
+
+
+@pytest.mark.parametrize("force,pattern", [("auto", b"error"), ("auto", b"^[a-j ]*error[a-j ]*$"),
+                                           ("table", b"error$")])
+def test_count_exact_when_capacity_too_small_with_parked_lines(gpu_ctx, force, pattern):
+    """dgrep_scan_device with a capacity below the match count (a size query:
+    0, or 1) must still return the exact number of matching lines when some
+    parked long lines do not match (dgrep.h: the count is exact)."""
+    import torch
+
+    sizes = [10, 300, 70000, 5, 1 << 20, 3 << 20, 40000, 9000, 100, (1 << 22) + 7, 2]
+    data = _long_split(9, sizes)
+    data = data + b"\n" + b"\n".join(b"x error %d" % i for i in range(500))
+    oln, _, _ = O.grep_map(pattern, data, threads=16)
+    n = len(data)
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    out = [torch.zeros(4, dtype=torch.int64, device="cuda") for _ in range(3)]
+    try:
+        gpu_ctx.set_stepper(force)
+        gpu_ctx.load(pattern)
+        for cap in (0, 1, 4):
+            cnt = gpu_ctx.scan_device(buf.data_ptr(), n, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), cap)
+            assert cnt == len(oln), (cap, cnt, len(oln))
+            assert gpu_ctx.scan_stats()["pending"] > 0
+    finally:
+        gpu_ctx.set_stepper("auto")

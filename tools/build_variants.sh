@@ -22,7 +22,8 @@ for spec in "$@"; do
       $HIPCC $FLAGS $defs -c "$P/csrc/runtime/dgrep_runtime.hip" -o "$P/build/dgrep_runtime_$name.o" 2>> "$P/build/variant_$name.log" &&
       $HIPCC -shared -fPIC --offload-arch=gfx950 -o "$P/variants/libdgrep_$name.so" \
         "$P"/build/go_parser.o "$P"/build/dfa_builder.o "$P"/build/compile_api.o "$P/build/scan_dfa_$name.o" \
-        "$P"/build/encode.o "$P"/build/reduce.o "$P/build/dgrep_runtime_$name.o" "$P"/build/build_info.o &&
+        "$P"/build/encode.o "$P"/build/reduce.o "$P/build/dgrep_runtime_$name.o" "$P"/build/exchange.o "$P"/build/build_info.o \
+        -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &&
       echo "built $name ($defs)"
   ) &
   pids+=($!)
