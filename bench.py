@@ -99,6 +99,8 @@ def parse():
                     help="full verification stops (and says how far it got) after this much wall time")
     ap.add_argument("--verify-windows", type=int, default=6)
     ap.add_argument("--lane-chunk", type=int, default=0, help="tuning: force the Sheng/pair/filter lane chunk (0 = adaptive)")
+    ap.add_argument("--base-offset", type=int, default=0,
+                    help="ablation: place the split this many bytes (a multiple of 64) into its HBM allocation")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the N-rank report (gloo, oracle instead of the GPU scan; value null)")
     ap.add_argument("--pattern", default=None,
@@ -238,7 +240,9 @@ def measure_gpu(args, wl, world, rank, local, dev, n, pattern, seed):
     cp = ctx.load(pattern)
 
     t = time.time()
-    buf = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+    off = args.base_offset - args.base_offset % 64
+    alloc = torch.empty(n + 64 + off, dtype=torch.uint8, device=dev)
+    buf = alloc[off:]
     ctx.synth(buf.data_ptr(), n, seed, wl["kind"])
     torch.cuda.synchronize(dev)
     log("rank %d: generated %.1f GiB split in %.1fs; DFA %d states x %d classes" %

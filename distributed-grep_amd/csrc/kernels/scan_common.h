@@ -71,7 +71,7 @@ constexpr uint32_t kNoNewline = 0xffffffffu;
 // the DFA over those bytes itself, from the state the earlier maps give.
 constexpr uint32_t kLazyNewline = 0xfffffffeu;
 #ifndef DGREP_LAZY_MAP_BYTES
-#define DGREP_LAZY_MAP_BYTES 0
+#define DGREP_LAZY_MAP_BYTES 256
 #endif
 constexpr uint32_t kLazyMapBytes = DGREP_LAZY_MAP_BYTES;  // a multiple of the Sheng block (0: maps from byte 0)
 

@@ -1098,11 +1098,13 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   else                                                                                     \
     run_block<BK, false>(st, M, V, pos, uint64_t(C), r, emit);
 #define DG_CHECK                                                                           \
-  if (kMap && kLazyMapBytes != 0 && maps && pos == kLazyMapBytes) {                        \
-    if (r.nl != 0u)                                                                        \
-      *emit.cmap = make_uint4(0u, 0u, kLazyNewline, 0u); /* resolved from the bytes */    \
-    else                                                                                   \
-      lazy_map(st, p, emit.mapsl);                                                         \
+  if constexpr (kMap && kLazyMapBytes != 0) {                                              \
+    if (maps && pos == kLazyMapBytes) {                                                    \
+      if (r.nl != 0u)                                                                      \
+        *emit.cmap = make_uint4(0u, 0u, kLazyNewline, 0u); /* resolved from the bytes */  \
+      else                                                                                 \
+        lazy_map(st, p, emit.mapsl);                                                       \
+    }                                                                                      \
   }                                                                                        \
   if (pos == uint64_t(C)) {                                                                \
     nl_chunk = r.nl;                                                                       \

@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
 for w in $WLS; do
   timeout -k 10 240 python bench.py --workload "$w" > "$O/bench_$w.json" 2> "$O/bench_$w.err"
 done

@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/abr_$TAG
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 for w in $WLS; do
   REPS=${REPS:-3} timeout -k 10 600 bash "$R/tools/variant_bench.sh" "$w" $VARS > "$OUT/$w.txt" 2>&1
 done

@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/q_$TAG
 mkdir -p "$OUT"
 cd "$R"
 if [ "$K" != "-" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" \
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread -k "$K" \
     > "$OUT/pytest_gpu.log" 2>&1
 fi
 for w in "$@"; do
