@@ -58,6 +58,11 @@ WORKLOADS = {
                       "lines, literal 'error'"),
     "long1g": dict(pattern="error", seed=8, kind=3, gib=16.0,
                    desc="long lines + one newline-free 1 GiB line: 16 GiB split (seed 8), literal 'error'"),
+    # config 4's 1,000-keyword pattern over long lines (kind 4: kind 2 with the
+    # keywords planted in filler pages and boundary lines): the filter stepper
+    "long_c4": dict(pattern=None, seed=4, kind=4, gib=16.0, verify_window=256 << 10,
+                    desc="long lines + C4 keywords: 16 GiB split (seed 4) of 4 MiB-mean lines between pages of log "
+                         "lines, (?i) alternation of 1,000 seeded keywords (filter stepper)"),
     # a dense Sheng line (~60 % of lines match): the lane chunk adapts to the match density
     "dense": dict(pattern="e", seed=2, kind=0, gib=16.0,
                   desc="dense: 16 GiB split (seed 2), literal 'e' (most lines match)"),
@@ -101,6 +106,8 @@ def parse():
     ap.add_argument("--lane-chunk", type=int, default=0, help="tuning: force the Sheng/pair/filter lane chunk (0 = adaptive)")
     ap.add_argument("--base-offset", type=int, default=0,
                     help="ablation: place the split this many bytes (a multiple of 64) into its HBM allocation")
+    ap.add_argument("--alloc-gib", type=float, default=0.0,
+                    help="ablation: allocate at least this many GiB for the split's buffer")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the N-rank report (gloo, oracle instead of the GPU scan; value null)")
     ap.add_argument("--pattern", default=None,
@@ -241,7 +248,7 @@ def measure_gpu(args, wl, world, rank, local, dev, n, pattern, seed):
 
     t = time.time()
     off = args.base_offset - args.base_offset % 64
-    alloc = torch.empty(n + 64 + off, dtype=torch.uint8, device=dev)
+    alloc = torch.empty(max(n + 64 + off, int(args.alloc_gib * (1 << 30))), dtype=torch.uint8, device=dev)
     buf = alloc[off:]
     ctx.synth(buf.data_ptr(), n, seed, wl["kind"])
     torch.cuda.synchronize(dev)

@@ -107,6 +107,11 @@
 #ifndef DGREP_PAIR_WAVES
 #define DGREP_PAIR_WAVES 3
 #endif
+// chunks per lane stepped in lockstep (2: two independent dependency chains
+// per lane, a fixed DGREP_PAIR_CHUNK, 2 waves per SIMD)
+#ifndef DGREP_PAIR_STREAMS
+#define DGREP_PAIR_STREAMS 1
+#endif
 // Filter (C4, > 256 states): one 1024-thread workgroup per CU shares one LDS image
 #ifndef DGREP_FILTER_CHUNK
 #define DGREP_FILTER_CHUNK 4096
@@ -291,51 +296,84 @@ struct StepWide {
 // states so that shadows, start_m and shadow(start_m) are the highest: a
 // pair-end state >= thr means an event -- at its first byte if it is a shadow
 // other than start_m, at its second byte if it is >= M (start_m or its shadow).
-struct StepPair {
+//
+// StepPairT<true> (kStepPairA, DFAs with K <= 16 classes): the same T2 image at
+// LDS kPairBaseA, below it a u8 PAIR-CLASS table PCT[b0 | b1 << 8] = c(b0) * K
+// + c(b1) for ASCII bytes (32 KiB; one 768-thread workgroup per CU shares it):
+// per word two ds_read_u8 (x & 0x7fff, bfe(x, 16, 15)) replace the four class
+// reads, and the chain is one v_lshl_add + one ds_read_u16 per pair. A word
+// with a byte >= 0x80 in any lane of the wave takes the UA/UB reads instead
+// (wave-uniform branch).
+template <bool PCT>
+struct StepPairT {
   static constexpr int kKind = kStepPair;
+  static constexpr bool kPct = PCT;
+  static constexpr uint32_t kBase = PCT ? kPairBaseA : 0u;  // UA, UB, then T2 at kBase + kPairT2
+  static constexpr uint32_t kT2 = kBase + kPairT2;
   const uint8_t* lds;
   const uint16_t* T1;
   uint32_t thr, M, div, K;
+  // PCT: a0 / a2 = c1 * K + c2 of the word's two pairs (b1, b3 unused);
+  // else a0 + b1 (a2 + b3) = 2 (c1 * K + c2), premultiplied byte tables
   struct Pre {
     uint32_t a0, b1, a2, b3;
   };
   __device__ __forceinline__ uint32_t ua(uint32_t b) const {
-    return *reinterpret_cast<const uint32_t*>(lds + 4u * b);
+    return *reinterpret_cast<const uint32_t*>(lds + kBase + 4u * b);
   }
   __device__ __forceinline__ uint32_t ub(uint32_t b) const {
-    return *reinterpret_cast<const uint32_t*>(lds + 1024u + 4u * b);
+    return *reinterpret_cast<const uint32_t*>(lds + kBase + 1024u + 4u * b);
   }
-  __device__ __forceinline__ Pre prep(uint32_t x) const {
+  __device__ __forceinline__ Pre prep_bytes(uint32_t x) const {
     // byte 0's table offset 4 * b0 as ONE v_lshlrev_b32_sdwa (hipcc emits
     // v_lshlrev + v_and for byte 0 while bytes 1-3 get the SDWA form)
     uint32_t o0;
     asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
         : "=v"(o0)
         : "v"(2u), "v"(x));
-    return Pre{*reinterpret_cast<const uint32_t*>(lds + o0), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu), ub(x >> 24)};
+    return Pre{*reinterpret_cast<const uint32_t*>(lds + kBase + o0), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu),
+               ub(x >> 24)};
+  }
+  __device__ __forceinline__ Pre prep(uint32_t x) const {
+    if constexpr (PCT) {
+      if (__builtin_expect(__ballot((x & 0x80808080u) != 0u) != 0ull, 0)) {
+        const Pre q = prep_bytes(x);
+        return Pre{(q.a0 + q.b1) >> 1, 0u, (q.a2 + q.b3) >> 1, 0u};
+      }
+      return Pre{lds[x & 0x7fffu], 0u, lds[__builtin_amdgcn_ubfe(x, 16u, 15u)], 0u};
+    } else {
+      return prep_bytes(x);
+    }
   }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
     return *reinterpret_cast<const uint16_t*>(lds + off);
   }
+  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const {
+    if constexpr (PCT) return t2((p.a0 << 1) + s);
+    return t2(s + p.a0 + p.b1);
+  }
+  __device__ __forceinline__ uint32_t second(const Pre& p, uint32_t s1) const {
+    if constexpr (PCT) return t2((p.a2 << 1) + s1);
+    return t2(s1 + p.a2 + p.b3);
+  }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
-    s1 = t2(s + p.a0 + p.b1);
-    s3 = t2(s1 + p.a2 + p.b3);
+    s1 = first(p, s);
+    s3 = second(p, s1);
     s0 = s1;
     s2 = s3;
   }
   // apply() in two parts: the word's first chain read, then the rest
-  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return t2(s + p.a0 + p.b1); }
   __device__ __forceinline__ void rest(const Pre& p, uint32_t f, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                        uint32_t& s3) const {
     s1 = f;
-    s3 = t2(s1 + p.a2 + p.b3);
+    s3 = second(p, s1);
     s0 = s1;
     s2 = s3;
   }
-  // single-byte step (rare paths): state id = (premultiplied state - kPairT2) / row bytes
+  // single-byte step (rare paths): state id = (premultiplied state - T2 base) / row bytes
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-    return T1[((s - kPairT2) / div) * K + (ub(b) >> 1)];
+    return T1[((s - kT2) / div) * K + (ub(b) >> 1)];
   }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
   __device__ __forceinline__ bool any2(uint32_t s1, uint32_t s3) const { return max(s1, s3) >= thr; }
@@ -345,6 +383,8 @@ struct StepPair {
            (uint32_t(s3 >= M) << 3);
   }
 };
+using StepPair = StepPairT<false>;
+using StepPairA = StepPairT<true>;
 
 // DFA of more than 256 states (large alternations, SURVEY config 4) as a
 // FILTER that lives wholly in LDS: the runtime keeps the DFA's shallowest
@@ -417,6 +457,11 @@ __device__ __forceinline__ StepPair make_step<StepPair>(const uint8_t* lds, cons
                   a.nclasses};
 }
 template <>
+__device__ __forceinline__ StepPairA make_step<StepPairA>(const uint8_t* lds, const ScanArgs& a) {
+  return StepPairA{lds, reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div,
+                   a.nclasses};
+}
+template <>
 __device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }
 template <>
 __device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds, const ScanArgs&) {
@@ -448,9 +493,9 @@ struct Tune<StepFilter> {
   static constexpr int C = DGREP_FILTER_CHUNK, E = DGREP_FILTER_SLOTS, B = DGREP_FILTER_BLOCK, S = 1;
 };
 static_assert(Tune<StepFilter>::C % Tune<StepFilter>::B == 0 && Tune<StepFilter>::C <= 32768, "bad filter chunk");
-template <>
-struct Tune<StepPair> {
-  static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = 1;
+template <bool P>
+struct Tune<StepPairT<P>> {
+  static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = DGREP_PAIR_STREAMS;
 };
 static_assert(Tune<StepPair>::B == 64 || Tune<StepPair>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepPair>::C % Tune<StepPair>::B == 0 && Tune<StepPair>::C <= 32768, "bad pair chunk");
@@ -653,7 +698,7 @@ constexpr bool sentinel() {
 template <class Step, bool DIRECT>
 constexpr bool flat_emit() {
   // (not Filter: its 1024 threads x 8 B dummy would not fit beside its 124 KiB image)
-  return !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair);
+  return !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair) && Tune<Step>::S == 1;
 }
 
 // Everything a word step does after its four DFA steps s0..s3 (newline mask
@@ -990,20 +1035,27 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
   r.nev = 0;
 }
 
-// The <= 256-state steppers park long lines in the main scan (slot mode; the
-// overflow pass re-runs chunks in direct mode and reads such a line on). The
-// filter's CAND state has no exact DFA state to resume from, and the wide
-// stepper is a forced test path: their lanes read a long line to its end.
+// The <= 256-state steppers and the filter park long lines in the main scan
+// (slot mode; the overflow pass stops at the same point). The filter's state
+// at the park point is not used (CAND has no exact DFA state): its parked
+// lines are decided from their start on the whole DFA (long_dfa_* kernels).
+// The wide stepper is a forced test path: its lanes read a long line to its end.
+#ifndef DGREP_FILTER_PARK
+#define DGREP_FILTER_PARK 1
+#endif
 template <class Step, bool DIRECT>
 constexpr bool track_long() {
-  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepTable) && !DIRECT;
+  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepTable ||
+          (Step::kKind == kStepFilter && DGREP_FILTER_PARK)) &&
+         !DIRECT;
 }
 // the parked state as an index of ScanArgs::pend_states (stepper encoding ->
 // DFA state of the blob)
 template <class Step>
 __device__ __forceinline__ uint32_t park_index(const ScanArgs& a, uint32_t s) {
   if constexpr (Step::kKind == kStepSheng8) return s & 0xffu;
-  else if constexpr (Step::kKind == kStepPair) return (s - kPairT2) / a.pair_div;
+  else if constexpr (Step::kKind == kStepPair) return (s - Step::kT2) / a.pair_div;
+  else if constexpr (Step::kKind == kStepFilter) return 0;  // re-run from the line start
   else return s;
 }
 
@@ -1290,6 +1342,13 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
       Emitter<E, false> e0{&a, slots, cs[0], 0, 0}, e1{&a, slots + E * 2, cs[1], 0, 0};
       e0.tail = tails;
       e1.tail = tails + 1;
+      if (a.spill) {
+        // one spill area per stream
+        uint2* sp0 = a.spill + ((uint64_t(blockIdx.x) * NT + uint64_t(tid)) * S) * a.spill_per_lane;
+        e0.spill = sp0;
+        e1.spill = sp0 + a.spill_per_lane;
+        e0.spill_cap = e1.spill_cap = a.spill_per_lane;
+      }
       if (full) {
         run_lane2<Tune<Step>::C, BK>(a, st, cs[0], cs[1], r[0], r[1], e0, e1, nlc[0], nlc[1]);
       } else {
@@ -1306,7 +1365,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         }
       }
       if (a.spill) {
-        em.spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane;
+        em.spill = a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * S * a.spill_per_lane;
         em.spill_cap = a.spill_per_lane;
       }
       nlc[0] = run_lane<BK>(a, st, cs[0], r[0], em, C);
@@ -1349,8 +1408,9 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
     for (int k = 0; k < S; ++k) {
       const uint32_t nev = r[k].nev;
       const uint32_t* sl = slots + k * E * 2;
-      const bool spill = S == 1 && a.spill;
-      const uint2* sp = spill ? a.spill + (uint64_t(blockIdx.x) * NT + uint64_t(tid)) * a.spill_per_lane : nullptr;
+      const bool spill = a.spill != nullptr;
+      const uint2* sp = spill ? a.spill + ((uint64_t(blockIdx.x) * NT + uint64_t(tid)) * S + k) * a.spill_per_lane
+                              : nullptr;
       const uint64_t o0 = base + ev_off[k];
       if (nev <= uint32_t(E) + (spill ? a.spill_per_lane : 0u)) {
         for (uint32_t j = 0; j < nev; ++j) {
@@ -1937,6 +1997,86 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
   }
 }
 
+// ---- long lines of the filter stepper (> 256 states) ---------------------------
+// A parked line is decided on the WHOLE DFA (breadth-first ids, u16/u32 table in
+// HBM with its leading rows in LDS, as verify_kernel) in parallel over its
+// bytes: the host cuts [line_start, end) into segments; long_dfa_seg_kernel
+// runs each segment on one lane from a GUESSED entry state -- the state the
+// DFA reaches from `start` over the kLongLookback bytes before the segment
+// (for keyword automata such as config 4's, the state after any 12+ bytes no
+// longer depends on what came before, so the guess is exact) -- and records
+// guess, exit state and whether the absorbing MATCHED state was reached;
+// long_dfa_fix_kernel then walks each line's segments in order from the true
+// state, takes a segment's exit when its guess was right and re-runs the
+// segment from the true state when it was not (exact for any DFA).
+constexpr uint32_t kLongLookback = 256;
+
+template <typename E>
+struct FullDfa {
+  const E* hot;  // LDS
+  const __attribute__((address_space(1))) E* full;
+  const uint32_t* cls;  // LDS
+  uint32_t K, hot_n;
+  __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t b) const {
+    const size_t i = size_t(s) * K + cls[b];
+    return i < hot_n ? uint32_t(hot[i]) : uint32_t(full[i]);
+  }
+  // state after bytes [a, e) from s, stopping at the absorbing `matched`
+  __device__ __forceinline__ uint32_t run(const uint8_t* data, uint64_t a, uint64_t e, uint32_t s,
+                                          uint32_t matched) const {
+    if (s == matched) return s;
+    for_line_bytes(data, a, e, [&](uint32_t b) {
+      s = next(s, b);
+      return s != matched;
+    });
+    return s;
+  }
+};
+
+template <typename E>
+__global__ __launch_bounds__(256) void long_dfa_seg_kernel(LongDfaArgs la) {
+  __shared__ uint32_t cls[256];
+  __shared__ __attribute__((aligned(16))) E hot[kVerifyHotBytes / sizeof(E)];
+  cls[threadIdx.x] = la.cls[threadIdx.x];
+  const E* full = static_cast<const E*>(la.full);
+  for (uint32_t i = threadIdx.x; i < la.hot_entries; i += 256) hot[i] = full[i];
+  __syncthreads();
+  const FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, la.hot_entries};
+  for (uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x; g < la.nseg; g += uint64_t(gridDim.x) * 256) {
+    const LongSeg sg = la.seg[g];
+    const uint64_t lb = la.seg_from[g];  // lookback start (the line start for its first segment)
+    const uint32_t guess = d.run(la.data, lb, sg.begin, la.start, la.matched);
+    la.seg_guess[g] = guess;
+    la.seg_exit[g] = d.run(la.data, sg.begin, sg.end, guess, la.matched);
+  }
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void long_dfa_fix_kernel(LongDfaArgs la) {
+  __shared__ uint32_t cls[256];
+  __shared__ __attribute__((aligned(16))) E hot[kVerifyHotBytes / sizeof(E)];
+  cls[threadIdx.x] = la.cls[threadIdx.x];
+  const E* full = static_cast<const E*>(la.full);
+  for (uint32_t i = threadIdx.x; i < la.hot_entries; i += 256) hot[i] = full[i];
+  __syncthreads();
+  const FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, la.hot_entries};
+  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < la.npend; i += uint64_t(gridDim.x) * 256) {
+    PendingLine P = la.pend[i];
+    uint32_t s = la.start;
+    for (uint64_t g = la.seg_off[i]; g < la.seg_off[i + 1] && s != la.matched; ++g) {
+      if (la.seg_guess[g] == s) {
+        s = la.seg_exit[g];
+      } else {
+        const LongSeg sg = la.seg[g];
+        s = d.run(la.data, sg.begin, sg.end, s, la.matched);
+      }
+    }
+    P.matched = (s == la.matched || d.next(s, uint32_t('\n')) == la.start_m) ? 1u : 0u;
+    P.len = P.end - P.line_start;
+    la.pend[i] = P;
+  }
+}
+
 template <uint32_t NW>
 __global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
   const NfaView g = nfa_view(v.nfa);
@@ -2032,6 +2172,9 @@ uint32_t scan_table_row() { return kRow; }
 namespace {
 template <class Step>
 constexpr int threads_of() {
+  if constexpr (Step::kKind == kStepPair) {
+    if constexpr (Step::kPct) return kPairAThreads;
+  }
   return Step::kKind == kStepWide ? kWideThreads : Step::kKind == kStepFilter ? kFilterThreads : kScanThreads;
 }
 template <class Step, int TBL>
@@ -2058,6 +2201,7 @@ hipError_t occ_t(int* b) {
 template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
+  if (kind == kStepPairA) return op.template run<StepPairA, int(kPairAImage)>();
   if (kind == kStepPair) {
     if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
     if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB)
@@ -2157,7 +2301,7 @@ uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t re
   (void)dispatch(kind, table_bytes,
                  TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots, spill_per_lane});
   *threads = *waves_per_block * 64;
-  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepFilter;
+  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepPairA || kind == kStepFilter;
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {
@@ -2206,6 +2350,28 @@ hipError_t long_lines_resolve(const LongArgs& la, hipStream_t stream) {
 hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream) {
   const uint64_t grid = la.npend < 4096 ? la.npend : 4096;
   if (grid) hipLaunchKernelGGL(long_sheng_kernel, dim3(grid), dim3(kLsThreads), 0, stream, la);
+  return hipGetLastError();
+}
+
+uint32_t long_lookback() { return kLongLookback; }
+
+hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
+  if (la.nseg) {
+    uint64_t grid = (la.nseg + 255) / 256;
+    if (grid > 65536) grid = 65536;
+    if (u32)
+      hipLaunchKernelGGL(long_dfa_seg_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, la);
+    else
+      hipLaunchKernelGGL(long_dfa_seg_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, la);
+  }
+  uint64_t grid = (la.npend + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  if (grid) {
+    if (u32)
+      hipLaunchKernelGGL(long_dfa_fix_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, la);
+    else
+      hipLaunchKernelGGL(long_dfa_fix_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, la);
+  }
   return hipGetLastError();
 }
 

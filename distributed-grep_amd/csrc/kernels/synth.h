@@ -14,7 +14,9 @@
 // word "error" in 1 page of 2048 -- so lines of consecutive filler pages,
 // 4 MiB long on average (geometric), alternate with a page of short lines;
 // kind 3 is kind 2 whose first 1 GiB holds no boundary page (one newline-free
-// line of 1 GiB plus the head of the next boundary page). Bytes are printable
+// line of 1 GiB plus the head of the next boundary page); kind 4 is kind 2 for
+// config 4: its boundary pages are kind-1 lines and a filler page plants one
+// of the seed's keywords (random case) instead of "error". Bytes are printable
 // ASCII plus '\n'. Any page can be regenerated alone, so a window of a 16 GiB
 // split can be checked on the CPU.
 #pragma once
@@ -132,11 +134,11 @@ DG_HD void line(uint64_t seed, uint64_t page, uint32_t li, int kind, char* o, ui
   o[end] = '\n';
 }
 
-// kinds 2 / 3: a filler page of a long line (no '\n')
-DG_HD void filler_page(uint64_t seed, uint64_t page, char* o, uint32_t bytes) {
+// kinds 2 / 3 / 4: a filler page of a long line (no '\n'); kw: plant a keyword
+DG_HD void filler_page(uint64_t seed, uint64_t page, char* o, uint32_t bytes, bool kw = false) {
   Rng r{mix(seed + 0xf111) ^ mix(page)};
   const bool plant = r.below(2048) == 0;
-  const uint32_t at = r.below(bytes > 8 ? bytes - 8 : 1);
+  const uint32_t at = r.below(bytes > 16 ? bytes - 16 : 1);
   uint32_t p = 0;
   while (p < bytes) {
     int wl;
@@ -144,22 +146,28 @@ DG_HD void filler_page(uint64_t seed, uint64_t page, char* o, uint32_t bytes) {
     for (int k = 0; k < wl && p < bytes; ++k) o[p++] = wd[k];
     if (p < bytes) o[p++] = ' ';
   }
-  if (plant)
+  if (plant && kw) {
+    Rng q{mix(seed + 0x6b77) ^ mix(page)};  // its own stream: kinds 2 / 3 unchanged
+    char w[16];
+    const int wl = keyword(seed, int(q.below(kKeywords)), w);
+    for (int k = 0; k < wl && at + uint32_t(k) < bytes; ++k) o[at + k] = q.below(2) ? char(w[k] - 32) : w[k];
+  } else if (plant) {
     for (int k = 0; k < 5 && at + uint32_t(k) < bytes; ++k) o[at + k] = "error"[k];
+  }
 }
 constexpr uint32_t kLongBoundary = 512;          // 1 page in 512 ends a long line
 constexpr uint64_t kLongFirstPages = (1u << 30) / kPage;  // kind 3: first 1 GiB
 
 // Fills page `page` (kPage bytes, or fewer for the split's last page: `bytes`).
 DG_HD void page_fill(uint64_t seed, uint64_t page, int kind, char* o, uint32_t bytes) {
-  if (kind == 2 || kind == 3) {
+  if (kind == 2 || kind == 3 || kind == 4) {
     const bool boundary = (mix(seed ^ 0xb0b0) ^ mix(page + 7)) % kLongBoundary == 0 &&
                           !(kind == 3 && page < kLongFirstPages);
     if (!boundary) {
-      filler_page(seed, page, o, bytes);
+      filler_page(seed, page, o, bytes, kind == 4);
       return;
     }
-    kind = 0;
+    kind = kind == 4 ? 1 : 0;
   }
   Rng r{mix(seed + 0x5151) ^ mix(page)};
   uint32_t p = 0, li = 0;

@@ -34,6 +34,10 @@
 #ifndef DGREP_PAIR_ENABLE
 #define DGREP_PAIR_ENABLE 1
 #endif
+// the pair stepper's ASCII pair-class table (kStepPairA) when it fits
+#ifndef DGREP_PAIR_PCT
+#define DGREP_PAIR_PCT 0
+#endif
 // matching-line records per resident thread of the HBM spill area the
 // one-chunk-per-lane steppers move full LDS slots to (0: no spilling)
 #ifndef DGREP_SPILL_RECORDS
@@ -44,6 +48,10 @@
 // and resolves through the per-chunk '\n' counts like the other steppers)
 #ifndef DGREP_PARK
 #define DGREP_PARK 1
+#endif
+// A/B knob: cap on the scan's resident workgroups per CU (the grid)
+#ifndef DGREP_MAX_WG_PER_CU
+#define DGREP_MAX_WG_PER_CU 64
 #endif
 #ifndef DGREP_SHENG_MAPS
 #define DGREP_SHENG_MAPS 1
@@ -65,6 +73,8 @@ hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t s
 hipError_t long_lines_end(const LongArgs& la, hipStream_t stream);
 hipError_t long_lines_resolve(const LongArgs& la, hipStream_t stream);
 hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream);
+hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream);
+uint32_t long_lookback();
 uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
@@ -142,6 +152,11 @@ struct dgrep_ctx {
   uint64_t seg_off_cap = 0;
   uint8_t* d_segmap = nullptr;
   uint64_t segmap_cap = 0;
+  // filter stepper: parked lines on the whole DFA (long_dfa_* kernels)
+  uint64_t* d_seg_from = nullptr;
+  uint64_t seg_from_cap = 0;
+  uint32_t* d_seg_state = nullptr;  // [2][nseg]: guess, exit
+  uint64_t seg_state_cap = 0;
 
   // dgrep_scan (host data) buffers
   uint8_t* d_data = nullptr;
@@ -224,7 +239,7 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 // start_m, then shadow(start_m): a pair-end id >= first shadow holds an
 // event. Returns false if the DFA does not fit (T2 > kPairMaxT2 bytes).
 bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::vector<uint8_t>* img, uint32_t* start,
-                      uint32_t* start_m, PairArgs* pa, std::vector<uint32_t>* orig_out) {
+                      uint32_t* start_m, PairArgs* pa, std::vector<uint32_t>* orig_out, uint32_t base = 0) {
   const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
   const uint32_t cn = h.byte_class[uint8_t('\n')];
   auto T = [&](uint32_t s, uint32_t c) { return trans[size_t(s) * K + c]; };
@@ -243,8 +258,9 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   // same column of different rows falls in different LDS banks
   const uint64_t row = ((2ull * K * K + 3) & ~3ull) | 4ull;
   if (row * Sp > kPairMaxT2) return false;
-  const uint64_t t1_off = (kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
-  if (end > kPairMaxImage) return false;
+  const uint64_t t1_off = (base + kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
+  if (end > (base ? uint64_t(kPairAImage) : uint64_t(kPairMaxImage))) return false;
+  if (base && K > 16) return false;  // PCT entries c1 * K + c2 must fit a byte
   std::vector<uint32_t> id(S), orig(Sp);
   uint32_t next = 0;
   for (uint32_t s = 0; s < S; ++s)
@@ -257,12 +273,18 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   if (m_shadow) { shadow_of[M] = next; orig[next++] = M; }
   // ids S-1 .. S'-1: the shadows of y != start_m, start_m, shadow(start_m)
   const uint32_t thr_id = S - 1;
-  auto premul = [&](uint32_t i) { return uint16_t(kPairT2 + uint64_t(i) * row); };
+  auto premul = [&](uint32_t i) { return uint16_t(base + kPairT2 + uint64_t(i) * row); };
   img->assign(end, 0);
-  uint32_t* ua = reinterpret_cast<uint32_t*>(img->data());
-  uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + 1024);
-  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data() + kPairT2);
+  uint32_t* ua = reinterpret_cast<uint32_t*>(img->data() + base);
+  uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + base + 1024);
+  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data() + base + kPairT2);
   uint16_t* t1 = reinterpret_cast<uint16_t*>(img->data() + t1_off);
+  if (base) {
+    // kStepPairA: PCT[b0 | b1 << 8] = c(b0) * K + c(b1) for ASCII b0, b1
+    for (uint32_t b0 = 0; b0 < 128; ++b0)
+      for (uint32_t b1 = 0; b1 < 128; ++b1)
+        (*img)[b0 | (b1 << 8)] = uint8_t(h.byte_class[b0] * K + h.byte_class[b1]);
+  }
   for (uint32_t i = 0; i < Sp; ++i) {
     const uint32_t x = orig[i];
     for (uint32_t c1 = 0; c1 < K; ++c1) {
@@ -404,7 +426,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
-                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
+                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_seg_from, c->d_seg_state, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -487,9 +509,13 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   std::vector<uint8_t> pair_img;
   uint32_t pair_start = 0, pair_m = 0;
   std::vector<uint32_t> st2id;  // stepper state index -> blob state (long lines, see resolve_long_lines)
-  const bool pair_ok = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3)
-                           ? build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args, &st2id)
-                           : false;
+  // the ASCII pair-class variant when its PCT fits (<= 16 classes, small image)
+  bool pair_pct = false;
+  const bool want_pair = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3);
+  if (want_pair && DGREP_PAIR_PCT)
+    pair_pct = build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args, &st2id, kPairBaseA);
+  const bool pair_ok = pair_pct || (want_pair && build_pair_image(h, trans, &pair_img, &pair_start, &pair_m,
+                                                                   &c->pair_args, &st2id));
   if (force == 3 && !pair_ok) {
     c->err = "dgrep_load_dfa: the pair stepper's two-byte table does not fit this DFA";
     return DGREP_E_UNSUPPORTED;
@@ -504,7 +530,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     return DGREP_E_UNSUPPORTED;
   }
   if (pair_ok) {
-    c->step_kind = kStepPair;
+    c->step_kind = pair_pct ? kStepPairA : kStepPair;
     c->nclasses = h.nclasses;
     t.swap(pair_img);
     start = pair_start;
@@ -662,7 +688,8 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_long_tbl = nullptr;
   c->d_st2id = nullptr;
   c->long_states = 0;
-  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepTable) && h.nstates <= 256 &&
+  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepPairA ||
+       c->step_kind == kStepTable) && h.nstates <= 256 &&
       !st2id.empty()) {
     std::vector<uint8_t> lt(size_t(h.nstates) * 256);
     for (uint32_t s = 0; s < h.nstates; ++s)
@@ -677,7 +704,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->empty_line_matches = trans[size_t(h.start) * h.nclasses + h.byte_class[uint8_t('\n')]] == h.start_m;
   int bpc = 0;
   HIPCHK(scan_dfa_occupancy(c->step_kind, c->table_bytes, &bpc));
-  c->blocks_per_cu = std::max(1, bpc);
+  c->blocks_per_cu = std::max(1, std::min(bpc, DGREP_MAX_WG_PER_CU));
   c->density = 0.0;
   c->staged_hint = 0;
   c->loaded = true;
@@ -734,6 +761,74 @@ static int resolve_long_lines(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, u
   return DGREP_OK;
 }
 
+// The filter stepper's parked lines (> 256 states): their ends from the chunk
+// '\n' counts, then each line decided on the whole DFA from its start, in
+// segments run in parallel from guessed entry states and checked in order
+// (long_dfa_* kernels in scan_dfa.hip). Segments of about 1/65536 of the
+// parked bytes (>= 64 KiB), so that the GPU fills with one lane per segment.
+static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64_t chunk, uint64_t nchunks,
+                               uint64_t npend) {
+  int rc;
+  LongArgs le;
+  memset(&le, 0, sizeof le);
+  le.data = d_data;
+  le.n = n;
+  le.chunk = chunk;
+  le.nchunks = nchunks;
+  le.chunk_nl = c->d_chunk_nl;
+  le.pend = c->d_pend;
+  le.npend = npend;
+  HIPCHK(long_lines_end(le, c->stream));
+  std::vector<PendingLine> P(npend);
+  HIPCHK(hipMemcpyAsync(P.data(), c->d_pend, npend * sizeof(PendingLine), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  uint64_t total = 0;
+  for (const PendingLine& p : P) total += p.end - p.line_start;
+  const uint64_t seg = std::max<uint64_t>(uint64_t(64) << 10, (total / 65536 + 15) & ~uint64_t(15));
+  std::vector<LongSeg> segs;
+  std::vector<uint64_t> from, off(npend + 1, 0);
+  const uint64_t lb = long_lookback();
+  for (uint64_t i = 0; i < npend; ++i) {
+    for (uint64_t b = P[i].line_start; b < P[i].end; b += seg) {
+      segs.push_back(LongSeg{b, std::min(P[i].end, b + seg)});
+      from.push_back(b - std::min(lb, b - P[i].line_start));
+    }
+    off[i + 1] = segs.size();
+  }
+  const uint64_t ns = std::max<uint64_t>(segs.size(), 1);
+  if ((rc = grow(c, &c->d_seg, &c->seg_cap, ns)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_seg_from, &c->seg_from_cap, ns)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_seg_state, &c->seg_state_cap, 2 * ns)) != DGREP_OK) return rc;
+  if ((rc = grow(c, &c->d_seg_off, &c->seg_off_cap, npend + 1)) != DGREP_OK) return rc;
+  if (!segs.empty()) {
+    HIPCHK(hipMemcpyAsync(c->d_seg, segs.data(), segs.size() * sizeof(LongSeg), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_seg_from, from.data(), from.size() * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(hipMemcpyAsync(c->d_seg_off, off.data(), off.size() * 8, hipMemcpyHostToDevice, c->stream));
+  LongDfaArgs la;
+  memset(&la, 0, sizeof la);
+  la.data = d_data;
+  la.full = c->d_full;
+  la.hot_entries = c->verify_hot;
+  la.nclasses = c->nclasses;
+  la.cls = c->d_cls;
+  la.start = c->blob_start;
+  la.start_m = c->blob_start_m;
+  la.matched = c->blob_matched;
+  la.seg = c->d_seg;
+  la.seg_from = c->d_seg_from;
+  la.nseg = segs.size();
+  la.seg_guess = c->d_seg_state;
+  la.seg_exit = c->d_seg_state + ns;
+  la.seg_off = c->d_seg_off;
+  la.pend = c->d_pend;
+  la.npend = npend;
+  HIPCHK(long_lines_dfa(la, c->full_u32, c->stream));
+  // the host vectors are read by the async copies above: wait before they go
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return DGREP_OK;
+}
+
 // Core of every scan: the split is resident at d_data (n bytes). Results go to
 // device arrays of `capacity` lines; *count receives the number of matches.
 static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64_t* d_line, uint64_t* d_start,
@@ -780,16 +875,20 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
 
   if (!c->d_overflow && (rc = grow(c, &c->d_overflow, &c->overflow_cap, 1u << 16)) != DGREP_OK) return rc;
   const int grid = int(std::min<uint64_t>(ntiles, resident));
+  // chunks per lane (the two-stream steppers step two in lockstep)
+  const uint32_t streams = tile / (uint64_t(kTileLanes) * chunk);
   const bool use_spill = spills && DGREP_SPILL_RECORDS > 0;
-  if (use_spill &&
-      (rc = grow(c, &c->d_spill, &c->spill_cap, uint64_t(grid) * threads * DGREP_SPILL_RECORDS)) != DGREP_OK)
+  if (use_spill && (rc = grow(c, &c->d_spill, &c->spill_cap,
+                              uint64_t(grid) * threads * streams * DGREP_SPILL_RECORDS)) != DGREP_OK)
     return rc;
   // long lines: the lanes' tail entries, '\n' per chunk and the pending list
   // (parking needs the blob's table: <= 256-state DFAs on the Sheng / pair /
   // table steppers)
-  const uint32_t streams = tile / (uint64_t(kTileLanes) * chunk);
   if ((rc = grow(c, &c->d_tails, &c->tails_cap, uint64_t(grid) * threads * streams)) != DGREP_OK) return rc;
-  const bool park = DGREP_PARK && c->d_long_tbl != nullptr;
+  // the filter parks too when the whole DFA is at hand (not a partial blob, whose
+  // candidates an NFA program decides: its lanes read a long line on)
+  const bool park_filter = DGREP_PARK && c->step_kind == kStepFilter && c->d_full != nullptr;
+  const bool park = (DGREP_PARK && c->d_long_tbl != nullptr) || park_filter;
   const uint64_t nchunks = (n + chunk - 1) / chunk;
   // Sheng: the chunk maps replace the '\n' counts (long_sheng_kernel)
   const bool park_maps = park && c->step_kind == kStepSheng8 && DGREP_SHENG_MAPS;
@@ -928,6 +1027,8 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
       la.sheng_v = reinterpret_cast<const uint2*>(c->d_table);
       la.data = d_data;
       HIPCHK(long_lines_sheng(la, c->stream));
+    } else if (npend && park_filter) {
+      if ((rc = resolve_long_filter(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) return rc;
     } else if (npend && (rc = resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) {
       return rc;
     }
@@ -962,7 +1063,8 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
       la.sheng_v = reinterpret_cast<const uint2*>(c->d_table);
       la.data = d_data;
       HIPCHK(long_lines_sheng(la, c->stream));
-    } else if ((rc = resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) {
+    } else if ((rc = park_filter ? resolve_long_filter(c, d_data, n, chunk, nchunks, npend)
+                                 : resolve_long_lines(c, d_data, n, chunk, nchunks, npend)) != DGREP_OK) {
       return rc;
     }
     HIPCHK(hipEventRecord(c->ev5, c->stream));

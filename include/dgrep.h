@@ -249,7 +249,9 @@ const char* dgrep_comm_last_error(dgrep_comm* comm);
 /* ---- bench / test tooling ------------------------------------------------ */
 /* Fill d_out[0:n) with the seeded synthetic log corpus on
  * the device. kind: 0 = plain log lines, 1 = log lines with seeded
- * case-insensitive keywords planted (config 4). */
+ * case-insensitive keywords planted (config 4), 2 = long lines (4 MiB mean)
+ * between pages of log lines, 3 = kind 2 after one newline-free 1 GiB line,
+ * 4 = kind 2 with config 4's keywords planted (csrc/kernels/synth.h). */
 int dgrep_synth_corpus(dgrep_ctx* ctx, void* d_out, size_t n, uint64_t seed, int kind);
 /* Host twin of dgrep_synth_corpus (same generator code): fills out[0:n). */
 int dgrep_synth_corpus_host(void* out, size_t n, uint64_t seed, int kind);

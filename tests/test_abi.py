@@ -101,3 +101,22 @@ def test_synth_long_line_kinds():
     assert (gaps < 300).sum() > 100          # and pages of log lines
     d3 = np.frombuffer(dgrep.synth_corpus_host(64 << 20, 3, 3), np.uint8)
     assert not (d3 == 10).any()
+
+
+def test_synth_kind4_plants_keywords_in_long_lines():
+    """kind 4 (bench workload long_c4): kind 2's long lines with config 4's
+    keywords planted (random case) in filler pages, and kind-1 boundary lines;
+    kind 2 itself is unchanged by it (same bytes as before the kind existed is
+    not checkable here, but kind 2 and 4 share every '\\n')."""
+    import numpy as np
+
+    n = 64 << 20
+    d4 = dgrep.synth_corpus_host(n, 4, 4)
+    d2 = dgrep.synth_corpus_host(n, 4, 2)
+    a4, a2 = np.frombuffer(d4, np.uint8), np.frombuffer(d2, np.uint8)
+    np.testing.assert_array_equal(np.flatnonzero(a4 == 10), np.flatnonzero(a2 == 10))
+    kws = dgrep.synth_keywords(4, 1000)
+    low = d4.lower()
+    found = sum(1 for k in kws if k in low)
+    assert found >= 3, found
+    assert bool(((a4 == 10) | ((a4 >= 0x20) & (a4 < 0x7f))).all())

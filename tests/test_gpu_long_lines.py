@@ -203,3 +203,49 @@ def test_count_exact_when_capacity_too_small_with_parked_lines(gpu_ctx, force, p
             assert gpu_ctx.scan_stats()["pending"] > 0
     finally:
         gpu_ctx.set_stepper("auto")
+
+
+def _c4_pattern(seed=4, nkw=1000):
+    import dgrep
+
+    return b"(?i)(" + b"|".join(dgrep.synth_keywords(seed, nkw)) + b")"
+
+
+def test_filter_long_lines_c4_keywords(gpu_ctx):
+    """Config 4's 1,000-keyword pattern (the filter stepper: > 256 DFA states)
+    over lines of 1-8 MiB, keywords planted in some (start, middle, end, mixed
+    case), between short log lines: bit-exact vs the oracle."""
+    import dgrep
+
+    kws = dgrep.synth_keywords(4, 1000)
+    rnd = random.Random(41)
+    words = [b"request", b"user", b"cache", b"latency", b"retry", b"shard", b"value", b"node"]
+    parts = []
+    for i in range(9):
+        L = rnd.randrange(1 << 20, 8 << 20)
+        body = bytearray(b" ".join(rnd.choice(words) for _ in range(L // 5))[:L])
+        where = i % 4
+        if where:
+            kw = bytearray(rnd.choice(kws))
+            for k in range(len(kw)):
+                if rnd.random() < 0.5:
+                    kw[k] -= 32
+            q = {1: 0, 2: L // 2, 3: L - len(kw)}[where]
+            body[q:q + len(kw)] = kw
+        parts.append(bytes(body))
+        parts.append(dgrep.synth_corpus_host(rnd.randrange(100, 20000), 300 + i, 1).rstrip(b"\n"))
+    data = b"\n".join(parts)
+    pattern = _c4_pattern()
+    st = _check(gpu_ctx, pattern, data)
+    assert st["stepper"] == "filter", st
+
+
+def test_filter_long_lines_synth_kind4(gpu_ctx):
+    """The long_c4 bench workload's corpus (synth kind 4) on the filter stepper,
+    24 MiB generated on the host, vs the oracle."""
+    import dgrep
+
+    data = dgrep.synth_corpus_host(24 << 20, 4, 4)
+    assert data.count(b"\n") < 10000  # mostly long lines
+    st = _check(gpu_ctx, _c4_pattern(), data)
+    assert st["stepper"] == "filter", st

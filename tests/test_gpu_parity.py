@@ -55,7 +55,7 @@ def _check(ctx, pattern, data, threads=1):
     return len(ln)
 
 
-@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
 def test_synth_device_matches_host(gpu_ctx, kind):
     import torch
     import dgrep
