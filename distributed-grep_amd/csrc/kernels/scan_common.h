@@ -122,6 +122,8 @@ struct ScanArgs {
   unsigned long long* pend_count;
   // Sheng stepper: the chunk maps instead of chunk_nl (nullptr: none)
   ChunkMap* chunk_map;
+  // tiles claimed after each wave's first (zeroed per launch)
+  unsigned long long* tile_next;
 };
 
 // the long-line kernels' arguments (long_end / long_map / long_fin)

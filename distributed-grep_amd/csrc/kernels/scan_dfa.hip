@@ -1307,6 +1307,19 @@ constexpr int waves_per_simd() {
                                                                   : kWideThreads / 256;  // one workgroup per CU
 }
 
+// the next tile for this wave: waves + (claims so far), wave-uniform
+// (DGREP_DYNAMIC_TILES 0: the static stride t + waves, for A/B)
+#ifndef DGREP_DYNAMIC_TILES
+#define DGREP_DYNAMIC_TILES 1
+#endif
+__device__ __forceinline__ uint64_t next_tile(const ScanArgs& a, uint64_t t, uint64_t waves) {
+  if (!DGREP_DYNAMIC_TILES) return t + waves;
+  uint64_t c = 0;
+  if ((threadIdx.x & 63u) == 0) c = atomicAdd(a.tile_next, 1ull);
+  const uint32_t lo = uint32_t(__shfl(uint32_t(c), 0, 64)), hi = uint32_t(__shfl(uint32_t(c >> 32), 0, 64));
+  return waves + ((uint64_t(hi) << 32) | lo);
+}
+
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
 // the tile's exclusive scans run on the wave's lanes (DPP/bpermute) and one
 // lane reserves the tile's staging range with a single atomic.
@@ -1330,7 +1343,13 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   const int lane = tid & 63;
   const uint64_t waves = uint64_t(gridDim.x) * (NT / 64);
   const uint64_t kTile = uint64_t(kTileLanes) * uint64_t(S) * uint64_t(C);
-  for (uint64_t t = uint64_t(blockIdx.x) * (NT / 64) + uint64_t(tid >> 6); t < a.ntiles; t += waves) {
+  // Tiles: the first one per wave by its index, every further one CLAIMED from
+  // a counter (one atomic per tile), so a wave that runs faster takes more
+  // tiles. Resident waves do not progress at one rate (the sequencer favours
+  // older waves): with a static stride the youngest waves set the kernel's
+  // end. Same box, C2 pattern: 12 / 18 / 32 GiB splits ran 9 % below 16 GiB,
+  // whose 2.67 rounds happened to give the young waves one tile less.
+  for (uint64_t t = uint64_t(blockIdx.x) * (NT / 64) + uint64_t(tid >> 6); t < a.ntiles; t = next_tile(a, t, waves)) {
     uint64_t cs[S];
     LaneRun r[S];
     uint32_t nlc[S];
@@ -2042,12 +2061,46 @@ __global__ __launch_bounds__(256) void long_dfa_seg_kernel(LongDfaArgs la) {
   for (uint32_t i = threadIdx.x; i < la.hot_entries; i += 256) hot[i] = full[i];
   __syncthreads();
   const FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, la.hot_entries};
-  for (uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x; g < la.nseg; g += uint64_t(gridDim.x) * 256) {
-    const LongSeg sg = la.seg[g];
-    const uint64_t lb = la.seg_from[g];  // lookback start (the line start for its first segment)
-    const uint32_t guess = d.run(la.data, lb, sg.begin, la.start, la.matched);
-    la.seg_guess[g] = guess;
-    la.seg_exit[g] = d.run(la.data, sg.begin, sg.end, guess, la.matched);
+  // two segments per lane (g and g + half), stepped byte by byte in lockstep:
+  // the chain is a dependent table read per byte, so two chains per lane
+  // overlap their latencies. Each runs [lookback start, end) from `start`
+  // and snapshots its state at the segment's begin (the guess). MATCHED is
+  // absorbing in the table, so no early stop is needed.
+  const uint64_t half = (la.nseg + 1) / 2;
+  for (uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x; g < half; g += uint64_t(gridDim.x) * 256) {
+    const uint64_t h = g + half;
+    const bool two = h < la.nseg;
+    const LongSeg A = la.seg[g];
+    const LongSeg B = two ? la.seg[h] : LongSeg{0, 0};
+    const uint64_t fa = la.seg_from[g], fb = two ? la.seg_from[h] : 0;
+    uint32_t sa = la.start, sb = la.start, ga = la.start, gb = la.start;
+    uint64_t qa = fa & ~uint64_t(15), qb = fb & ~uint64_t(15);
+    while (qa < A.end || qb < B.end) {
+      const bool la_ = qa < A.end, lb_ = qb < B.end;
+      const uint4 va = la_ ? *reinterpret_cast<const uint4*>(la.data + qa) : make_uint4(0, 0, 0, 0);
+      const uint4 vb = lb_ ? *reinterpret_cast<const uint4*>(la.data + qb) : make_uint4(0, 0, 0, 0);
+      const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint64_t pa = qa + uint64_t(j), pb = qb + uint64_t(j);
+        if (pa == A.begin) ga = sa;
+        if (pb == B.begin) gb = sb;
+        const uint32_t ba = (wa[j >> 2] >> (8 * (j & 3))) & 0xffu, bb = (wb[j >> 2] >> (8 * (j & 3))) & 0xffu;
+        const uint32_t na = d.next(sa, ba), nb = d.next(sb, bb);
+        sa = (pa >= fa && pa < A.end) ? na : sa;
+        sb = (pb >= fb && pb < B.end) ? nb : sb;
+      }
+      qa += 16;
+      qb += 16;
+    }
+    if (A.begin == fa) ga = la.start;  // no lookback: the line's first segment
+    if (B.begin == fb) gb = la.start;
+    la.seg_guess[g] = ga;
+    la.seg_exit[g] = sa;
+    if (two) {
+      la.seg_guess[h] = gb;
+      la.seg_exit[h] = sb;
+    }
   }
 }
 
@@ -2088,11 +2141,11 @@ __global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
 // compute, per tile, its first output index (exclusive scan of counts) and the
 // 1-based number of its first line (1 + exclusive scan of newline counts), then
 // copy every tile's lines to their final place in split order.
-// The scan of the per-tile counts is ONE workgroup (a 16 GiB split at 32 KiB
-// chunks is 8,192 tiles = 128 KiB of TileInfo: 8 per thread, one pass), so the
+// The scan of the per-tile counts is ONE workgroup (a 16 GiB split at 16 KiB
+// chunks is 16,384 tiles = 256 KiB of TileInfo: 16 per thread, one pass), so the
 // ordering is two launches: tile_scan_kernel, order_lines_kernel.
 constexpr int kTsThreads = 1024;
-constexpr int kTsPer = 8;
+constexpr int kTsPer = 16;  // 16,384 tiles in one pass (C3's 16 KiB chunks: 31 -> ~16 us per split)
 
 __global__ __launch_bounds__(kTsThreads) void tile_scan_kernel(const TileInfo* tiles, uint64_t ntiles,
                                                                uint64_t* out_off, uint64_t* line_base) {
@@ -2357,7 +2410,7 @@ uint32_t long_lookback() { return kLongLookback; }
 
 hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
   if (la.nseg) {
-    uint64_t grid = (la.nseg + 255) / 256;
+    uint64_t grid = ((la.nseg + 1) / 2 + 255) / 256;
     if (grid > 65536) grid = 65536;
     if (u32)
       hipLaunchKernelGGL(long_dfa_seg_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, la);

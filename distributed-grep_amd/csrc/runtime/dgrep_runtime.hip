@@ -80,6 +80,8 @@ uint32_t verify_hot_bytes();
 
 using namespace dgrep;
 
+constexpr size_t kCounters = 8;
+
 // StepPair image offsets and thresholds (see StepPair in scan_dfa.hip)
 struct PairArgs {
   uint32_t t1 = 0, thr = 0, div = 0;
@@ -126,7 +128,8 @@ struct dgrep_ctx {
   uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0;
   StagedLine* d_staging = nullptr;
   uint64_t staging_cap = 0;
-  // device counters: [0] staging append counter, [1] overflow lanes, [2] status bits
+  // device counters: [0] staging append counter, [1] overflow lanes, [2] parked
+  // lines, [3] dropped candidates, [4] claimed tiles
   unsigned long long* d_counters = nullptr;
   OverflowLane* d_overflow = nullptr;
   uint64_t overflow_cap = 0;
@@ -409,7 +412,7 @@ extern "C" int dgrep_open(int device, dgrep_ctx** out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev3);
   if (e == hipSuccess) e = hipEventCreate(&c->ev4);
   if (e == hipSuccess) e = hipEventCreate(&c->ev5);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), kCounters * sizeof(unsigned long long));
   if (e != hipSuccess) {
     // keep the context so the caller can read the message
     c->err = std::string("dgrep_open: ") + hipGetErrorString(e);
@@ -764,8 +767,8 @@ static int resolve_long_lines(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, u
 // The filter stepper's parked lines (> 256 states): their ends from the chunk
 // '\n' counts, then each line decided on the whole DFA from its start, in
 // segments run in parallel from guessed entry states and checked in order
-// (long_dfa_* kernels in scan_dfa.hip). Segments of about 1/65536 of the
-// parked bytes (>= 64 KiB), so that the GPU fills with one lane per segment.
+// (long_dfa_* kernels in scan_dfa.hip). Segments sized so that every resident
+// lane gets about four (two at a time, stepped in lockstep), >= 16 KiB.
 static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64_t chunk, uint64_t nchunks,
                                uint64_t npend) {
   int rc;
@@ -784,7 +787,8 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   HIPCHK(hipStreamSynchronize(c->stream));
   uint64_t total = 0;
   for (const PendingLine& p : P) total += p.end - p.line_start;
-  const uint64_t seg = std::max<uint64_t>(uint64_t(64) << 10, (total / 65536 + 15) & ~uint64_t(15));
+  // about four segments per resident lane (two per lane per round), >= 16 KiB
+  const uint64_t seg = std::max<uint64_t>(uint64_t(16) << 10, (total / (uint64_t(c->num_cus) * 3072) + 15) & ~uint64_t(15));
   std::vector<LongSeg> segs;
   std::vector<uint64_t> from, off(npend + 1, 0);
   const uint64_t lb = long_lookback();
@@ -915,6 +919,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.tiles = c->d_tiles;
   a.overflow_count = c->d_counters + 1;
   a.pend_count = c->d_counters + 2;
+  a.tile_next = c->d_counters + 4;
   a.tails = c->d_tails;
   a.chunk_nl = park && !park_maps ? c->d_chunk_nl : nullptr;
   a.chunk_map = park_maps ? c->d_chunk_map : nullptr;
@@ -950,7 +955,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     a.overflow_cap = c->overflow_cap;
     a.pend = park ? c->d_pend : nullptr;
     a.pend_cap = park ? c->pend_cap : 0;
-    HIPCHK(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, kCounters * sizeof(unsigned long long), c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     HIPCHK(scan_dfa(c->step_kind, a, grid, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
