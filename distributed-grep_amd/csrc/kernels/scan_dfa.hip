@@ -1312,6 +1312,9 @@ constexpr int waves_per_simd() {
 #ifndef DGREP_DYNAMIC_TILES
 #define DGREP_DYNAMIC_TILES 1
 #endif
+#ifndef DGREP_PRIO_MODE
+#define DGREP_PRIO_MODE 0
+#endif
 __device__ __forceinline__ uint64_t next_tile(const ScanArgs& a, uint64_t t, uint64_t waves) {
   if (!DGREP_DYNAMIC_TILES) return t + waves;
   uint64_t c = 0;
@@ -1338,6 +1341,13 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   __syncthreads();
 
   const Step st = make_step<Step>(sm.tbl, a);
+  if constexpr (DGREP_PRIO_MODE == 1) {
+    // A/B: raise the priority of younger workgroups (dispatched later, so
+    // behind in the sequencer's age order): 0 for the first third of the grid
+    const uint32_t pr = blockIdx.x * 3u / gridDim.x;
+    if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pr >= 2) __builtin_amdgcn_s_setprio(2);
+  }
   constexpr int S = streams_of<Step, TBL>();  // chunks per lane: chunk k of a tile is k * 64 + lane
   uint32_t* slots = sm.slots + tid * ES * 2;
   const int lane = tid & 63;
@@ -2052,46 +2062,60 @@ struct FullDfa {
   }
 };
 
+// one 1024-thread workgroup per CU holds the DFA's first kLongDfaHotBytes of
+// rows (breadth-first: the states keyword text spends its bytes in; C4's
+// depth <= 3 rows need ~110 KiB) -- the segment lanes' table reads stay in LDS
+constexpr int kLongDfaThreads = 1024;
+constexpr uint32_t kLongDfaHotBytes = 120 * 1024;
+
 template <typename E>
-__global__ __launch_bounds__(256) void long_dfa_seg_kernel(LongDfaArgs la) {
+__global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg_kernel(LongDfaArgs la) {
   __shared__ uint32_t cls[256];
-  __shared__ __attribute__((aligned(16))) E hot[kVerifyHotBytes / sizeof(E)];
-  cls[threadIdx.x] = la.cls[threadIdx.x];
+  __shared__ __attribute__((aligned(16))) E hot[kLongDfaHotBytes / sizeof(E)];
+  if (threadIdx.x < 256) cls[threadIdx.x] = la.cls[threadIdx.x];
   const E* full = static_cast<const E*>(la.full);
-  for (uint32_t i = threadIdx.x; i < la.hot_entries; i += 256) hot[i] = full[i];
+  const uint32_t hot_n = min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
+  for (uint32_t i = threadIdx.x; i < hot_n; i += kLongDfaThreads) hot[i] = full[i];
   __syncthreads();
-  const FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, la.hot_entries};
+  const FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, hot_n};
   // two segments per lane (g and g + half), stepped byte by byte in lockstep:
   // the chain is a dependent table read per byte, so two chains per lane
   // overlap their latencies. Each runs [lookback start, end) from `start`
   // and snapshots its state at the segment's begin (the guess). MATCHED is
   // absorbing in the table, so no early stop is needed.
   const uint64_t half = (la.nseg + 1) / 2;
-  for (uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x; g < half; g += uint64_t(gridDim.x) * 256) {
+  for (uint64_t g = uint64_t(blockIdx.x) * kLongDfaThreads + threadIdx.x; g < half;
+       g += uint64_t(gridDim.x) * kLongDfaThreads) {
     const uint64_t h = g + half;
     const bool two = h < la.nseg;
     const LongSeg A = la.seg[g];
     const LongSeg B = two ? la.seg[h] : LongSeg{0, 0};
     const uint64_t fa = la.seg_from[g], fb = two ? la.seg_from[h] : 0;
     uint32_t sa = la.start, sb = la.start, ga = la.start, gb = la.start;
-    uint64_t qa = fa & ~uint64_t(15), qb = fb & ~uint64_t(15);
-    while (qa < A.end || qb < B.end) {
-      const bool la_ = qa < A.end, lb_ = qb < B.end;
-      const uint4 va = la_ ? *reinterpret_cast<const uint4*>(la.data + qa) : make_uint4(0, 0, 0, 0);
-      const uint4 vb = lb_ ? *reinterpret_cast<const uint4*>(la.data + qb) : make_uint4(0, 0, 0, 0);
+    // 32-bit positions relative to each run's 16-aligned start; the next
+    // 16-byte piece of both runs is loaded while this one is stepped
+    const uint64_t ba0 = fa & ~uint64_t(15), bb0 = fb & ~uint64_t(15);
+    const uint32_t lo_a = uint32_t(fa - ba0), beg_a = uint32_t(A.begin - ba0), end_a = uint32_t(A.end - ba0);
+    const uint32_t lo_b = uint32_t(fb - bb0), beg_b = two ? uint32_t(B.begin - bb0) : 0u,
+                   end_b = two ? uint32_t(B.end - bb0) : 0u;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 na4 = end_a ? *reinterpret_cast<const uint4*>(la.data + ba0) : z;
+    uint4 nb4 = end_b ? *reinterpret_cast<const uint4*>(la.data + bb0) : z;
+    for (uint32_t q = 0; q < end_a || q < end_b; q += 16) {
+      const uint4 va = na4, vb = nb4;
+      na4 = q + 16 < end_a ? *reinterpret_cast<const uint4*>(la.data + ba0 + q + 16) : z;
+      nb4 = q + 16 < end_b ? *reinterpret_cast<const uint4*>(la.data + bb0 + q + 16) : z;
       const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const uint64_t pa = qa + uint64_t(j), pb = qb + uint64_t(j);
-        if (pa == A.begin) ga = sa;
-        if (pb == B.begin) gb = sb;
-        const uint32_t ba = (wa[j >> 2] >> (8 * (j & 3))) & 0xffu, bb = (wb[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        const uint32_t na = d.next(sa, ba), nb = d.next(sb, bb);
-        sa = (pa >= fa && pa < A.end) ? na : sa;
-        sb = (pb >= fb && pb < B.end) ? nb : sb;
+        const uint32_t p = q + uint32_t(j);
+        if (p == beg_a) ga = sa;
+        if (p == beg_b) gb = sb;
+        const uint32_t xa = (wa[j >> 2] >> (8 * (j & 3))) & 0xffu, xb = (wb[j >> 2] >> (8 * (j & 3))) & 0xffu;
+        const uint32_t na = d.next(sa, xa), nb = d.next(sb, xb);
+        sa = (p >= lo_a && p < end_a) ? na : sa;
+        sb = (p >= lo_b && p < end_b) ? nb : sb;
       }
-      qa += 16;
-      qb += 16;
     }
     if (A.begin == fa) ga = la.start;  // no lookback: the line's first segment
     if (B.begin == fb) gb = la.start;
@@ -2289,10 +2313,20 @@ constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
 #ifndef DGREP_PAIR_MAX_CHUNK
 #define DGREP_PAIR_MAX_CHUNK 16384
 #endif
+// Doubling also stops below DGREP_MIN_TILES_X2 / 2 tiles per resident wave
+// (Sheng, pair; the filter keeps 1):
+// with tiles claimed dynamically, a split of exactly 2 tiles per wave ran 7 %
+// slower than 4 tiles of half the chunk (12 GiB: 32 KiB 4,462-4,580 GB/s,
+// 16 KiB 5,152), while 2.67 (16 GiB) and 5.33 (32 GiB) tiles per wave at
+// 32 KiB beat 16 KiB (profiles/r04/ablation/chunk_dyn.txt).
+#ifndef DGREP_MIN_TILES_X2
+#define DGREP_MIN_TILES_X2 5
+#endif
 uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c, uint64_t dens_cap,
-                              uint64_t max_c = kShengMaxChunk) {
+                              uint64_t max_c = kShengMaxChunk, uint64_t min_tiles_x2 = DGREP_MIN_TILES_X2) {
   uint64_t c = floor_c;
-  while (c * 2 <= max_c && n >= waves * uint64_t(kTileLanes) * c * 2 && (!dens_cap || c * 2 <= dens_cap))
+  while (c * 2 <= max_c && 2 * n >= min_tiles_x2 * waves * uint64_t(kTileLanes) * c * 2 &&
+         (!dens_cap || c * 2 <= dens_cap))
     c *= 2;
   return uint32_t(c);
 }
@@ -2319,7 +2353,9 @@ struct TileOp {
     if constexpr (adaptive_chunk<S, T>())
       c = force ? uint64_t(force)
                 : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap,
-                                       S::kKind == kStepPair ? DGREP_PAIR_MAX_CHUNK : kShengMaxChunk);
+                                       S::kKind == kStepPair ? DGREP_PAIR_MAX_CHUNK : kShengMaxChunk,
+                                       // the filter keeps 32 KiB at 2 tiles per wave (C4: 16 KiB -1.5 %)
+                                       S::kKind == kStepFilter ? 2 : DGREP_MIN_TILES_X2);
     *chunk = uint32_t(c);
     *waves_per_block = uint32_t(threads_of<S>() / 64);
     *bytes = uint64_t(kTileLanes) * uint64_t(streams_of<S, T>()) * c;
@@ -2407,15 +2443,16 @@ hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream) {
 }
 
 uint32_t long_lookback() { return kLongLookback; }
+uint32_t long_dfa_hot_bytes() { return kLongDfaHotBytes; }
 
 hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
   if (la.nseg) {
-    uint64_t grid = ((la.nseg + 1) / 2 + 255) / 256;
+    uint64_t grid = ((la.nseg + 1) / 2 + kLongDfaThreads - 1) / kLongDfaThreads;
     if (grid > 65536) grid = 65536;
     if (u32)
-      hipLaunchKernelGGL(long_dfa_seg_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, la);
+      hipLaunchKernelGGL(long_dfa_seg_kernel<uint32_t>, dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
     else
-      hipLaunchKernelGGL(long_dfa_seg_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, la);
+      hipLaunchKernelGGL(long_dfa_seg_kernel<uint16_t>, dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
   }
   uint64_t grid = (la.npend + 255) / 256;
   if (grid > 4096) grid = 4096;

@@ -75,6 +75,7 @@ hipError_t long_lines_resolve(const LongArgs& la, hipStream_t stream);
 hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream);
 hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream);
 uint32_t long_lookback();
+uint32_t long_dfa_hot_bytes();
 uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
@@ -814,6 +815,10 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   la.data = d_data;
   la.full = c->d_full;
   la.hot_entries = c->verify_hot;
+  {
+    const size_t esz = c->full_u32 ? 4 : 2, ne = size_t(c->nstates) * c->nclasses;
+    la.seg_hot_entries = uint32_t(std::min<size_t>(ne, long_dfa_hot_bytes() / esz)) / c->nclasses * c->nclasses;
+  }
   la.nclasses = c->nclasses;
   la.cls = c->d_cls;
   la.start = c->blob_start;

@@ -239,18 +239,19 @@ def test_overflow_pass_dense_table(gpu_ctx, pattern):
 
 
 def test_adaptive_chunk_on_large_split_and_density_cap(gpu_ctx):
-    """The adaptive Sheng chunk on a 2 GiB HBM-resident split (large enough to
-    select more than the compiled 4 KiB: dgrep_last_scan_stats reports it),
+    """The adaptive Sheng chunk on a 6 GiB HBM-resident split (large enough to
+    select more than the compiled 4 KiB at >= 2.5 tiles per resident wave:
+    dgrep_last_scan_stats reports it),
     then a dense pattern: after its first scan the match density caps the
     chunk. Every record is checked structurally and evenly spaced windows
     (split start and end included) against the oracle (bench.verify_windows)."""
     import torch
     import bench
 
-    n = 2 << 30
+    n = 6 << 30
     buf = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     gpu_ctx.synth(buf.data_ptr(), n, 21, 0)
-    cap = 40 << 20
+    cap = 100 << 20
     ln = torch.empty(cap, dtype=torch.int64, device="cuda")
     st = torch.empty(cap, dtype=torch.int64, device="cuda")
     le = torch.empty(cap, dtype=torch.int64, device="cuda")
