@@ -2176,15 +2176,17 @@ __global__ __launch_bounds__(kTsThreads) void tile_scan_kernel(const TileInfo* t
   __shared__ unsigned long long wc[kTsThreads / 64], wl[kTsThreads / 64];
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   unsigned long long carry_c = 0, carry_l = 0;
-  for (uint64_t t0 = 0; t0 < ntiles; t0 += uint64_t(kTsThreads) * kTsPer) {
-    const uint64_t b = t0 + uint64_t(threadIdx.x) * kTsPer;
+  // tiles per thread: as few as cover the split in one pass (at most kTsPer)
+  const uint32_t per = uint32_t(min<uint64_t>(kTsPer, max<uint64_t>(1, (ntiles + kTsThreads - 1) / kTsThreads)));
+  for (uint64_t t0 = 0; t0 < ntiles; t0 += uint64_t(kTsThreads) * per) {
+    const uint64_t b = t0 + uint64_t(threadIdx.x) * per;
     uint32_t c[kTsPer], l[kTsPer];
     unsigned long long sc = 0, sl = 0;
 #pragma unroll
     for (int i = 0; i < kTsPer; ++i) {
       c[i] = 0;
       l[i] = 0;
-      if (b + i < ntiles) {
+      if (uint32_t(i) < per && b + i < ntiles) {
         const TileInfo ti = tiles[b + i];
         c[i] = ti.count;
         l[i] = ti.nl;
@@ -2209,7 +2211,7 @@ __global__ __launch_bounds__(kTsThreads) void tile_scan_kernel(const TileInfo* t
     __syncthreads();  // wc / wl are rewritten by the next round
 #pragma unroll
     for (int i = 0; i < kTsPer; ++i) {
-      if (b + i < ntiles) {
+      if (uint32_t(i) < per && b + i < ntiles) {
         out_off[b + i] = pc;
         line_base[b + i] = pl + 1;
       }
