@@ -41,10 +41,10 @@
 //   * Matching lines are parked in per-lane LDS slots, counted, then the tile's
 //     lines are appended to a staging buffer with ONE atomic per tile, in
 //     ascending order inside the tile (no workgroup barrier anywhere: waves
-//     are independent). Two small passes (tile_scan_kernel: one workgroup's
-//     exclusive scan of the per-tile counts; order_lines_kernel: a wave per
-//     tile) turn tile-relative line numbers into global ones and lay the
-//     tiles out in split order.
+//     are independent). Two small passes (tile_block_sum_kernel: sums per
+//     64 tiles; order_lines_kernel: a wave per tile adds the sums before it)
+//     turn tile-relative line numbers into global ones and lay the tiles out
+//     in split order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -505,7 +505,12 @@ static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>:
               "chunk must be a multiple of the block");
 // the LDS slots pack a matching line's chunk-relative start and '\n' index in
 // 16 bits each (Emitter): no compiled or runtime chunk may exceed 32 KiB
-constexpr int kMaxLaneChunk = 32768;
+// (start < C and rel <= start, so 16 bits hold both up to C = 64 KiB)
+#ifndef DGREP_MAX_LANE_CHUNK
+#define DGREP_MAX_LANE_CHUNK 32768
+#endif
+constexpr int kMaxLaneChunk = DGREP_MAX_LANE_CHUNK;
+static_assert(kMaxLaneChunk <= 65536, "16-bit slot offsets");
 static_assert(Tune<StepSheng8>::C <= kMaxLaneChunk && Tune<StepTable>::C <= kMaxLaneChunk &&
                   Tune<StepWide>::C <= kMaxLaneChunk,
               "lane chunk above 32 KiB overflows the 16-bit LDS slot offsets");
@@ -668,7 +673,7 @@ struct Blk {
 // with one shift and "the lane owns the line" is lnl != 0 (0: the lane has not
 // crossed a '\n' yet). Blocks past the chunk end start from kLnlSeen (owned,
 // previous '\n' in r.prev_nl: q there may lie further back than kLnlOff).
-constexpr uint32_t kLnlOff = 1u << 17;  // > 2 * 32 KiB: any q >= -(C + 1) inside the chunk
+constexpr uint32_t kLnlOff = 1u << 17;  // > C + 1 for any C <= 64 KiB: any q >= -(C + 1) inside the chunk
 constexpr uint32_t kLnlBase = 8u * (3u + kLnlOff);  // lnl >= kLnlBase: a '\n' inside this block
 constexpr uint32_t kLnlSeen = 8u;
 template <int J>
@@ -2162,77 +2167,66 @@ __global__ __launch_bounds__(256) void verify_nfa_kernel(VerifyArgs v) {
 
 // ---- ordering passes ------------------------------------------------------
 // Tiles append their lines to the staging buffer in atomic order; these passes
-// compute, per tile, its first output index (exclusive scan of counts) and the
-// 1-based number of its first line (1 + exclusive scan of newline counts), then
-// copy every tile's lines to their final place in split order.
-// The scan of the per-tile counts is ONE workgroup (a 16 GiB split at 16 KiB
-// chunks is 16,384 tiles = 256 KiB of TileInfo: 16 per thread, one pass), so the
-// ordering is two launches: tile_scan_kernel, order_lines_kernel.
-constexpr int kTsThreads = 1024;
-constexpr int kTsPer = 16;  // 16,384 tiles in one pass (C3's 16 KiB chunks: 31 -> ~16 us per split)
+// place every tile's lines at its final output index (exclusive prefix of the
+// per-tile counts) with the 1-based number of its first line (1 + exclusive
+// prefix of the per-tile '\n' counts), in split order. tile_block_sum_kernel
+// reduces each block of 64 tiles (one wave per block: 128 blocks for a 16 GiB
+// split at 32 KiB chunks); order_lines_kernel (one wave per tile) adds the block
+// sums before its block and the tiles of its block before it, then copies. Two
+// launches either way: a single-workgroup scan of all tile counts took 16-100 us
+// per split (it is latency-bound on one CU), the block sums ~2 us.
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
 
-__global__ __launch_bounds__(kTsThreads) void tile_scan_kernel(const TileInfo* tiles, uint64_t ntiles,
-                                                               uint64_t* out_off, uint64_t* line_base) {
-  __shared__ unsigned long long wc[kTsThreads / 64], wl[kTsThreads / 64];
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  unsigned long long carry_c = 0, carry_l = 0;
-  // tiles per thread: as few as cover the split in one pass (at most kTsPer)
-  const uint32_t per = uint32_t(min<uint64_t>(kTsPer, max<uint64_t>(1, (ntiles + kTsThreads - 1) / kTsThreads)));
-  for (uint64_t t0 = 0; t0 < ntiles; t0 += uint64_t(kTsThreads) * per) {
-    const uint64_t b = t0 + uint64_t(threadIdx.x) * per;
-    uint32_t c[kTsPer], l[kTsPer];
-    unsigned long long sc = 0, sl = 0;
-#pragma unroll
-    for (int i = 0; i < kTsPer; ++i) {
-      c[i] = 0;
-      l[i] = 0;
-      if (uint32_t(i) < per && b + i < ntiles) {
-        const TileInfo ti = tiles[b + i];
-        c[i] = ti.count;
-        l[i] = ti.nl;
-      }
-      sc += c[i];
-      sl += l[i];
+__global__ __launch_bounds__(256) void tile_block_sum_kernel(const TileInfo* tiles, uint64_t ntiles, uint64_t* bsum_c,
+                                                             uint64_t* bsum_l) {
+  const uint64_t nb = (ntiles + 63) / 64;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t b = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); b < nb; b += uint64_t(gridDim.x) * 4) {
+    const uint64_t t = b * 64 + lane;
+    uint64_t c = 0, l = 0;
+    if (t < ntiles) {
+      const TileInfo ti = tiles[t];
+      c = ti.count;
+      l = ti.nl;
     }
-    unsigned long long ic = sc, il = sl;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const unsigned long long xc = __shfl_up(ic, d, 64), xl = __shfl_up(il, d, 64);
-      if (lane >= uint32_t(d)) { ic += xc; il += xl; }
-    }
-    if (lane == 63) { wc[w] = ic; wl[w] = il; }
-    __syncthreads();
-    unsigned long long pc = carry_c + ic - sc, pl = carry_l + il - sl;
-    for (uint32_t j = 0; j < kTsThreads / 64; ++j) {
-      if (j < w) { pc += wc[j]; pl += wl[j]; }
-      carry_c += wc[j];
-      carry_l += wl[j];
-    }
-    __syncthreads();  // wc / wl are rewritten by the next round
-#pragma unroll
-    for (int i = 0; i < kTsPer; ++i) {
-      if (uint32_t(i) < per && b + i < ntiles) {
-        out_off[b + i] = pc;
-        line_base[b + i] = pl + 1;
-      }
-      pc += c[i];
-      pl += l[i];
+    c = wave_sum_u64(c);
+    l = wave_sum_u64(l);
+    if (lane == 0) {
+      bsum_c[b] = c;
+      bsum_l[b] = l;
     }
   }
 }
 
-// one wave per tile copies its staged lines to their final slots (SoA)
+// one wave per tile: its prefix, then its staged lines copied to their final slots (SoA)
 __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles, const StagedLine* staging,
-                                                          uint64_t ntiles, const uint64_t* out_off,
-                                                          const uint64_t* line_base, uint64_t staging_cap,
+                                                          uint64_t ntiles, const uint64_t* bsum_c,
+                                                          const uint64_t* bsum_l, uint64_t staging_cap,
                                                           uint64_t capacity, uint64_t* line_no, uint64_t* start,
                                                           uint64_t* len) {
   const uint64_t waves = uint64_t(gridDim.x) * 4;
+  const uint32_t lane = threadIdx.x & 63u;
   for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles; t += waves) {
     const TileInfo ti = tiles[t];
     if (ti.count == 0) continue;
-    const uint64_t o = out_off[t], lb = line_base[t];
-    for (uint32_t k = threadIdx.x & 63; k < ti.count; k += 64) {
+    const uint64_t b = t / 64;
+    uint64_t pc = 0, pl = 0;
+    for (uint64_t j = lane; j < b; j += 64) {
+      pc += bsum_c[j];
+      pl += bsum_l[j];
+    }
+    const uint64_t tt = b * 64 + lane;
+    if (tt < t) {
+      const TileInfo x = tiles[tt];
+      pc += x.count;
+      pl += x.nl;
+    }
+    const uint64_t o = wave_sum_u64(pc), lb = wave_sum_u64(pl) + 1;
+    for (uint32_t k = lane; k < ti.count; k += 64) {
       const uint64_t src = ti.base + k, dst = o + k;
       if (src < staging_cap && dst < capacity) {
         const StagedLine L = staging[src];
@@ -2247,6 +2241,7 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
 // ---- host-side launchers (called from dgrep_runtime.cpp) ----------------
 
 uint32_t scan_table_row() { return kRow; }
+uint32_t scan_max_lane_chunk() { return uint32_t(kMaxLaneChunk); }
 
 namespace {
 template <class Step>
@@ -2405,11 +2400,14 @@ hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStr
   return dispatch(kind, a.table_bytes, OverflowOp{&a, nover, stream});
 }
 
-// out_off / line_base: ntiles entries each
+// out_off / line_base: scratch of ceil(ntiles / 64) entries each (block sums)
 hipError_t order_lines(const TileInfo* tiles, const StagedLine* staging, uint64_t ntiles, uint64_t* out_off,
                        uint64_t* line_base, uint64_t staging_cap, uint64_t capacity, uint64_t* line_no,
                        uint64_t* start, uint64_t* len, hipStream_t stream) {
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kTsThreads), 0, stream, tiles, ntiles, out_off, line_base);
+  // out_off / line_base hold the 64-tile block sums (ceil(ntiles / 64) each)
+  const uint64_t nb = (ntiles + 63) / 64;
+  const uint64_t bgrid = std::min<uint64_t>((nb + 3) / 4, 4096);
+  if (bgrid) hipLaunchKernelGGL(tile_block_sum_kernel, dim3(bgrid), dim3(256), 0, stream, tiles, ntiles, out_off, line_base);
   uint64_t grid = (ntiles + 3) / 4;
   if (grid > 16384) grid = 16384;
   hipLaunchKernelGGL(order_lines_kernel, dim3(grid), dim3(256), 0, stream, tiles, staging, ntiles, out_off,

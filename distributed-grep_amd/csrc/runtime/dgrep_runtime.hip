@@ -63,6 +63,7 @@ uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t re
                          double density, uint32_t spill_per_lane, uint32_t* chunk, uint32_t* waves_per_block,
                          uint32_t* slots, uint32_t* threads, bool* spills);
 uint32_t scan_table_row();
+uint32_t scan_max_lane_chunk();
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu);
 hipError_t scan_dfa(int kind, const ScanArgs& a, int grid, hipStream_t stream);
 hipError_t scan_dfa_overflow(int kind, const ScanArgs& a, uint64_t nover, hipStream_t stream);
@@ -467,8 +468,8 @@ extern "C" int dgrep_set_stream(dgrep_ctx* c, void* s) {
 
 extern "C" int dgrep_set_lane_chunk(dgrep_ctx* c, uint32_t chunk_bytes) {
   if (!c) return DGREP_E_INVALID;
-  if (chunk_bytes && (chunk_bytes % 128 || chunk_bytes < 4096 || chunk_bytes > 32768)) {
-    c->err = "lane chunk must be 0 or a multiple of 128 in [4096, 32768]";
+  if (chunk_bytes && (chunk_bytes % 128 || chunk_bytes < 4096 || chunk_bytes > scan_max_lane_chunk())) {
+    c->err = "lane chunk must be 0 or a multiple of 128 in [4096, " + std::to_string(scan_max_lane_chunk()) + "]";
     return DGREP_E_INVALID;
   }
   c->lane_chunk = chunk_bytes;
