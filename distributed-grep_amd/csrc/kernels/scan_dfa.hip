@@ -505,12 +505,9 @@ static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>:
               "chunk must be a multiple of the block");
 // the LDS slots pack a matching line's chunk-relative start and '\n' index in
 // 16 bits each (Emitter): no compiled or runtime chunk may exceed 32 KiB
-// (start < C and rel <= start, so 16 bits hold both up to C = 64 KiB)
-#ifndef DGREP_MAX_LANE_CHUNK
-#define DGREP_MAX_LANE_CHUNK 32768
-#endif
-constexpr int kMaxLaneChunk = DGREP_MAX_LANE_CHUNK;
-static_assert(kMaxLaneChunk <= 65536, "16-bit slot offsets");
+// (a 64 KiB build -- start < C and rel <= start still fit 16 bits -- failed the
+// 32 GiB C5 full-split parity in round 4 and was not pursued)
+constexpr int kMaxLaneChunk = 32768;
 static_assert(Tune<StepSheng8>::C <= kMaxLaneChunk && Tune<StepTable>::C <= kMaxLaneChunk &&
                   Tune<StepWide>::C <= kMaxLaneChunk,
               "lane chunk above 32 KiB overflows the 16-bit LDS slot offsets");
@@ -717,9 +714,12 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
 // read BEFORE the next word's class reads (`pf`). LDS reads complete in order,
 // so a chain read issued after them also waits for them. Same-box A/B: C4
 // kernel 3,678 -> 3,773 GB/s; the pair stepper (C3) lost 2.6 % with it.
+#ifndef DGREP_CHAIN_FIRST_KINDS
+#define DGREP_CHAIN_FIRST_KINDS (1 << kStepFilter)
+#endif
 template <class Step>
 constexpr bool chain_first() {
-  return Step::kKind == kStepFilter;
+  return ((DGREP_CHAIN_FIRST_KINDS) >> Step::kKind) & 1;
 }
 // sched_barrier mask: everything but LDS instructions may cross
 constexpr int kSchedNoDs = 0x7f;

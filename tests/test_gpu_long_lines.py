@@ -70,13 +70,9 @@ def test_long_lines_parked_and_resolved(gpu_ctx, force, pattern):
         gpu_ctx.set_stepper("auto")
 
 
-@pytest.mark.parametrize("chunk", [4096, 8192, 32768, 65536])
+@pytest.mark.parametrize("chunk", [4096, 8192, 32768])
 def test_long_lines_at_chunk_edges(gpu_ctx, chunk):
     """Lines ending exactly at chunk boundaries and at 2 C (the parking point)."""
-    import dgrep
-
-    if chunk == 65536 and "DGREP_MAX_LANE_CHUNK=65536" not in dgrep.build_info():
-        pytest.skip("lane chunks above 32 KiB not built (DGREP_MAX_LANE_CHUNK)")
     gpu_ctx.set_lane_chunk(chunk)
     try:
         for extra in (-1, 0, 1):

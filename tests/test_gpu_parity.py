@@ -107,18 +107,10 @@ def test_tile_and_chunk_boundaries(gpu_ctx, size):
 # splits (dgrep_set_lane_chunk forces them at oracle-friendly sizes): chunk and
 # tile edges, lines longer than a chunk, and more matching lines per lane than
 # LDS slots (pattern "" matches every line: the overflow kernel)
-def _max_lane_chunk():
-    import dgrep
-
-    return 65536 if "DGREP_MAX_LANE_CHUNK=65536" in dgrep.build_info() else 32768
-
-
-@pytest.mark.parametrize("chunk", [4224, 8192, 14592, 16384, 32768, 65536])
+@pytest.mark.parametrize("chunk", [4224, 8192, 14592, 16384, 32768])
 def test_sheng_adaptive_chunks(gpu_ctx, chunk):
     import dgrep
 
-    if chunk > _max_lane_chunk():
-        pytest.skip("lane chunks above 32 KiB not built (DGREP_MAX_LANE_CHUNK)")
     tile = 64 * chunk
     try:
         gpu_ctx.set_lane_chunk(chunk)
@@ -142,8 +134,7 @@ def test_sheng_adaptive_chunks(gpu_ctx, chunk):
 def test_lane_chunk_validation(gpu_ctx):
     import dgrep
 
-    bad_sizes = (100, 4000, 4097, 65664, 1 << 20) + ((32896, 65536) if _max_lane_chunk() == 32768 else ())
-    for bad in bad_sizes:
+    for bad in (100, 4000, 4097, 32896, 65536, 1 << 20):
         with pytest.raises(dgrep.DgrepError):
             gpu_ctx.set_lane_chunk(bad)
     gpu_ctx.set_lane_chunk(0)
