@@ -215,7 +215,6 @@ enum : int {
   kStepWide = 2,    // <= 65535 states: u16 [state][class] table, hot rows in LDS, all rows in HBM
   kStepPair = 3,    // 2 * states * classes^2 <= kPairMaxT2 bytes: two input bytes per table lookup
   kStepFilter = 4,  // > 256 states: the DFA's shallow part in LDS, lines that leave it verified afterwards
-  kStepPairA = 5,   // the pair stepper with a u8 pair-class table for ASCII bytes (<= 16 classes)
 };
 
 // LDS image of kStepFilter: byte classes [256] (u8), then u16 [state][class]
@@ -240,13 +239,6 @@ constexpr uint32_t kFilterClassBytes = 256;
 constexpr uint32_t kPairMaxT2 = 32768;
 constexpr uint32_t kPairMaxImage = 40960;
 constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the byte tables)
-// kStepPairA: the u8 pair-class table PCT at LDS 0 (index b0 | b1 << 8 of two
-// ASCII bytes: 0x7f80 entries), the pair image above it at kPairBaseA; one
-// workgroup of kPairAThreads per CU shares it. The pair image may then take at
-// most kPairAImage - kPairBaseA bytes (its premultiplied u16 states stay < 64 Ki).
-constexpr uint32_t kPairBaseA = 32768;
-constexpr uint32_t kPairAImage = kPairBaseA + 16384;
-constexpr int kPairAThreads = 768;
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
 // runtime renumbers states hottest-first (start, start_m, then BFS order from

@@ -296,25 +296,15 @@ struct StepWide {
 // states so that shadows, start_m and shadow(start_m) are the highest: a
 // pair-end state >= thr means an event -- at its first byte if it is a shadow
 // other than start_m, at its second byte if it is >= M (start_m or its shadow).
-//
-// StepPairT<true> (kStepPairA, DFAs with K <= 16 classes): the same T2 image at
-// LDS kPairBaseA, below it a u8 PAIR-CLASS table PCT[b0 | b1 << 8] = c(b0) * K
-// + c(b1) for ASCII bytes (32 KiB; one 768-thread workgroup per CU shares it):
-// per word two ds_read_u8 (x & 0x7fff, bfe(x, 16, 15)) replace the four class
-// reads, and the chain is one v_lshl_add + one ds_read_u16 per pair. A word
-// with a byte >= 0x80 in any lane of the wave takes the UA/UB reads instead
-// (wave-uniform branch).
-template <bool PCT>
-struct StepPairT {
+
+struct StepPair {
   static constexpr int kKind = kStepPair;
-  static constexpr bool kPct = PCT;
-  static constexpr uint32_t kBase = PCT ? kPairBaseA : 0u;  // UA, UB, then T2 at kBase + kPairT2
+  static constexpr uint32_t kBase = 0u;  // UA, UB, then T2 at kPairT2
   static constexpr uint32_t kT2 = kBase + kPairT2;
   const uint8_t* lds;
   const uint16_t* T1;
   uint32_t thr, M, div, K;
-  // PCT: a0 / a2 = c1 * K + c2 of the word's two pairs (b1, b3 unused);
-  // else a0 + b1 (a2 + b3) = 2 (c1 * K + c2), premultiplied byte tables
+  // a0 + b1 (a2 + b3) = 2 (c1 * K + c2): premultiplied byte tables
   struct Pre {
     uint32_t a0, b1, a2, b3;
   };
@@ -334,28 +324,12 @@ struct StepPairT {
     return Pre{*reinterpret_cast<const uint32_t*>(lds + kBase + o0), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu),
                ub(x >> 24)};
   }
-  __device__ __forceinline__ Pre prep(uint32_t x) const {
-    if constexpr (PCT) {
-      if (__builtin_expect(__ballot((x & 0x80808080u) != 0u) != 0ull, 0)) {
-        const Pre q = prep_bytes(x);
-        return Pre{(q.a0 + q.b1) >> 1, 0u, (q.a2 + q.b3) >> 1, 0u};
-      }
-      return Pre{lds[x & 0x7fffu], 0u, lds[__builtin_amdgcn_ubfe(x, 16u, 15u)], 0u};
-    } else {
-      return prep_bytes(x);
-    }
-  }
+  __device__ __forceinline__ Pre prep(uint32_t x) const { return prep_bytes(x); }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
     return *reinterpret_cast<const uint16_t*>(lds + off);
   }
-  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const {
-    if constexpr (PCT) return t2((p.a0 << 1) + s);
-    return t2(s + p.a0 + p.b1);
-  }
-  __device__ __forceinline__ uint32_t second(const Pre& p, uint32_t s1) const {
-    if constexpr (PCT) return t2((p.a2 << 1) + s1);
-    return t2(s1 + p.a2 + p.b3);
-  }
+  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return t2(s + p.a0 + p.b1); }
+  __device__ __forceinline__ uint32_t second(const Pre& p, uint32_t s1) const { return t2(s1 + p.a2 + p.b3); }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
     s1 = first(p, s);
@@ -383,8 +357,6 @@ struct StepPairT {
            (uint32_t(s3 >= M) << 3);
   }
 };
-using StepPair = StepPairT<false>;
-using StepPairA = StepPairT<true>;
 
 // DFA of more than 256 states (large alternations, SURVEY config 4) as a
 // FILTER that lives wholly in LDS: the runtime keeps the DFA's shallowest
@@ -456,11 +428,7 @@ __device__ __forceinline__ StepPair make_step<StepPair>(const uint8_t* lds, cons
   return StepPair{lds, reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div,
                   a.nclasses};
 }
-template <>
-__device__ __forceinline__ StepPairA make_step<StepPairA>(const uint8_t* lds, const ScanArgs& a) {
-  return StepPairA{lds, reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div,
-                   a.nclasses};
-}
+
 template <>
 __device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }
 template <>
@@ -493,8 +461,8 @@ struct Tune<StepFilter> {
   static constexpr int C = DGREP_FILTER_CHUNK, E = DGREP_FILTER_SLOTS, B = DGREP_FILTER_BLOCK, S = 1;
 };
 static_assert(Tune<StepFilter>::C % Tune<StepFilter>::B == 0 && Tune<StepFilter>::C <= 32768, "bad filter chunk");
-template <bool P>
-struct Tune<StepPairT<P>> {
+template <>
+struct Tune<StepPair> {
   static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = DGREP_PAIR_STREAMS;
 };
 static_assert(Tune<StepPair>::B == 64 || Tune<StepPair>::B == 128, "block must be 64 or 128 bytes");
@@ -1317,9 +1285,6 @@ constexpr int waves_per_simd() {
 #ifndef DGREP_DYNAMIC_TILES
 #define DGREP_DYNAMIC_TILES 1
 #endif
-#ifndef DGREP_PRIO_MODE
-#define DGREP_PRIO_MODE 0
-#endif
 __device__ __forceinline__ uint64_t next_tile(const ScanArgs& a, uint64_t t, uint64_t waves) {
   if (!DGREP_DYNAMIC_TILES) return t + waves;
   uint64_t c = 0;
@@ -1346,13 +1311,6 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   __syncthreads();
 
   const Step st = make_step<Step>(sm.tbl, a);
-  if constexpr (DGREP_PRIO_MODE == 1) {
-    // A/B: raise the priority of younger workgroups (dispatched later, so
-    // behind in the sequencer's age order): 0 for the first third of the grid
-    const uint32_t pr = blockIdx.x * 3u / gridDim.x;
-    if (pr == 1) __builtin_amdgcn_s_setprio(1);
-    else if (pr >= 2) __builtin_amdgcn_s_setprio(2);
-  }
   constexpr int S = streams_of<Step, TBL>();  // chunks per lane: chunk k of a tile is k * 64 + lane
   uint32_t* slots = sm.slots + tid * ES * 2;
   const int lane = tid & 63;
@@ -2246,9 +2204,6 @@ uint32_t scan_max_lane_chunk() { return uint32_t(kMaxLaneChunk); }
 namespace {
 template <class Step>
 constexpr int threads_of() {
-  if constexpr (Step::kKind == kStepPair) {
-    if constexpr (Step::kPct) return kPairAThreads;
-  }
   return Step::kKind == kStepWide ? kWideThreads : Step::kKind == kStepFilter ? kFilterThreads : kScanThreads;
 }
 template <class Step, int TBL>
@@ -2275,7 +2230,6 @@ hipError_t occ_t(int* b) {
 template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
   if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
-  if (kind == kStepPairA) return op.template run<StepPairA, int(kPairAImage)>();
   if (kind == kStepPair) {
     if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
     if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB)
@@ -2387,7 +2341,7 @@ uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t re
   (void)dispatch(kind, table_bytes,
                  TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots, spill_per_lane});
   *threads = *waves_per_block * 64;
-  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepPairA || kind == kStepFilter;
+  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepFilter;
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {

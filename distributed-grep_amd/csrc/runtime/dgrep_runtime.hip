@@ -34,10 +34,6 @@
 #ifndef DGREP_PAIR_ENABLE
 #define DGREP_PAIR_ENABLE 1
 #endif
-// the pair stepper's ASCII pair-class table (kStepPairA) when it fits
-#ifndef DGREP_PAIR_PCT
-#define DGREP_PAIR_PCT 0
-#endif
 // matching-line records per resident thread of the HBM spill area the
 // one-chunk-per-lane steppers move full LDS slots to (0: no spilling)
 #ifndef DGREP_SPILL_RECORDS
@@ -244,7 +240,7 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 // start_m, then shadow(start_m): a pair-end id >= first shadow holds an
 // event. Returns false if the DFA does not fit (T2 > kPairMaxT2 bytes).
 bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::vector<uint8_t>* img, uint32_t* start,
-                      uint32_t* start_m, PairArgs* pa, std::vector<uint32_t>* orig_out, uint32_t base = 0) {
+                      uint32_t* start_m, PairArgs* pa, std::vector<uint32_t>* orig_out) {
   const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
   const uint32_t cn = h.byte_class[uint8_t('\n')];
   auto T = [&](uint32_t s, uint32_t c) { return trans[size_t(s) * K + c]; };
@@ -263,9 +259,8 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   // same column of different rows falls in different LDS banks
   const uint64_t row = ((2ull * K * K + 3) & ~3ull) | 4ull;
   if (row * Sp > kPairMaxT2) return false;
-  const uint64_t t1_off = (base + kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
-  if (end > (base ? uint64_t(kPairAImage) : uint64_t(kPairMaxImage))) return false;
-  if (base && K > 16) return false;  // PCT entries c1 * K + c2 must fit a byte
+  const uint64_t t1_off = (kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
+  if (end > kPairMaxImage) return false;
   std::vector<uint32_t> id(S), orig(Sp);
   uint32_t next = 0;
   for (uint32_t s = 0; s < S; ++s)
@@ -278,18 +273,12 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   if (m_shadow) { shadow_of[M] = next; orig[next++] = M; }
   // ids S-1 .. S'-1: the shadows of y != start_m, start_m, shadow(start_m)
   const uint32_t thr_id = S - 1;
-  auto premul = [&](uint32_t i) { return uint16_t(base + kPairT2 + uint64_t(i) * row); };
+  auto premul = [&](uint32_t i) { return uint16_t(kPairT2 + uint64_t(i) * row); };
   img->assign(end, 0);
-  uint32_t* ua = reinterpret_cast<uint32_t*>(img->data() + base);
-  uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + base + 1024);
-  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data() + base + kPairT2);
+  uint32_t* ua = reinterpret_cast<uint32_t*>(img->data());
+  uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + 1024);
+  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data() + kPairT2);
   uint16_t* t1 = reinterpret_cast<uint16_t*>(img->data() + t1_off);
-  if (base) {
-    // kStepPairA: PCT[b0 | b1 << 8] = c(b0) * K + c(b1) for ASCII b0, b1
-    for (uint32_t b0 = 0; b0 < 128; ++b0)
-      for (uint32_t b1 = 0; b1 < 128; ++b1)
-        (*img)[b0 | (b1 << 8)] = uint8_t(h.byte_class[b0] * K + h.byte_class[b1]);
-  }
   for (uint32_t i = 0; i < Sp; ++i) {
     const uint32_t x = orig[i];
     for (uint32_t c1 = 0; c1 < K; ++c1) {
@@ -514,13 +503,8 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   std::vector<uint8_t> pair_img;
   uint32_t pair_start = 0, pair_m = 0;
   std::vector<uint32_t> st2id;  // stepper state index -> blob state (long lines, see resolve_long_lines)
-  // the ASCII pair-class variant when its PCT fits (<= 16 classes, small image)
-  bool pair_pct = false;
   const bool want_pair = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3);
-  if (want_pair && DGREP_PAIR_PCT)
-    pair_pct = build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args, &st2id, kPairBaseA);
-  const bool pair_ok = pair_pct || (want_pair && build_pair_image(h, trans, &pair_img, &pair_start, &pair_m,
-                                                                   &c->pair_args, &st2id));
+  const bool pair_ok = want_pair && build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args, &st2id);
   if (force == 3 && !pair_ok) {
     c->err = "dgrep_load_dfa: the pair stepper's two-byte table does not fit this DFA";
     return DGREP_E_UNSUPPORTED;
@@ -535,7 +519,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     return DGREP_E_UNSUPPORTED;
   }
   if (pair_ok) {
-    c->step_kind = pair_pct ? kStepPairA : kStepPair;
+    c->step_kind = kStepPair;
     c->nclasses = h.nclasses;
     t.swap(pair_img);
     start = pair_start;
@@ -693,8 +677,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_long_tbl = nullptr;
   c->d_st2id = nullptr;
   c->long_states = 0;
-  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepPairA ||
-       c->step_kind == kStepTable) && h.nstates <= 256 &&
+  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepTable) && h.nstates <= 256 &&
       !st2id.empty()) {
     std::vector<uint8_t> lt(size_t(h.nstates) * 256);
     for (uint32_t s = 0; s < h.nstates; ++s)

@@ -60,7 +60,7 @@ EXPORTS = (
 )
 COMM_ID_BYTES = 128
 
-STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair", 4: "filter", 5: "pair"}  # 5: pair + ASCII pair-class table
+STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair", 4: "filter"}
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
 
