@@ -9,6 +9,7 @@
 //                by index and later ones claimed from a counter
 // Build: hipcc -O3 --offload-arch=gfx950 tools/pattern_ceiling.hip -o tools/pattern_ceiling
 // Run:   tools/pattern_ceiling [GiB ...]     (prints one line per size and kernel)
+//        env PC_LDS (LDS bytes per workgroup), PC_C (lane chunk), PC_DEPTH (128-B blocks in flight, 1-3)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -40,6 +41,7 @@ __global__ __launch_bounds__(kThreads) void coalesced(const uint4* __restrict__ 
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+template <int DEPTH>
 __global__ __launch_bounds__(kThreads, 3) void lanechunk(const uint8_t* __restrict__ d, uint64_t n, uint32_t C,
                                                         unsigned long long* next, uint32_t* out) {
   extern __shared__ uint32_t pad[];  // kLds bytes at launch: 3 workgroups per CU
@@ -50,18 +52,23 @@ __global__ __launch_bounds__(kThreads, 3) void lanechunk(const uint8_t* __restri
   uint32_t acc = pad[0];
   for (uint64_t t = uint64_t(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); t < ntiles;) {
     const uint4* p = reinterpret_cast<const uint4*>(d + t * tile + uint64_t(lane) * C);
-    uint4 A[8], B[8];
+    // DEPTH blocks of 128 B in flight ahead of the one being consumed
+    uint4 Q[DEPTH + 1][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) A[i] = p[i];
+    for (int k = 0; k < DEPTH; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) Q[k][i] = p[k * 8 + i];
     const uint32_t nb = C / 128;
     for (uint32_t b = 0; b < nb; ++b) {
-      const uint32_t nx = b + 1 < nb ? b + 1 : b;
+      const uint32_t nx = b + DEPTH < nb ? b + DEPTH : nb - 1;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) B[i] = p[nx * 8 + i];
+      for (int i = 0; i < 8; ++i) Q[DEPTH][i] = p[nx * 8 + i];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc ^= A[i].x ^ A[i].y ^ A[i].z ^ A[i].w;
+      for (int i = 0; i < 8; ++i) acc ^= Q[0][i].x ^ Q[0][i].y ^ Q[0][i].z ^ Q[0][i].w;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) A[i] = B[i];
+      for (int k = 0; k < DEPTH; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) Q[k][i] = Q[k + 1][i];
     }
     uint64_t c = 0;
     if (lane == 0) c = atomicAdd(next, 1ull);
@@ -75,8 +82,10 @@ int main(int argc, char** argv) {
   CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   int occ = 0;
   const size_t lds = argc > 1 && getenv("PC_LDS") ? size_t(atoi(getenv("PC_LDS"))) : size_t(kLds);
-  CHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lanechunk, kThreads, lds));
-  const uint32_t C = 32768;
+  const int depth = getenv("PC_DEPTH") ? atoi(getenv("PC_DEPTH")) : 1;
+  auto kern = depth == 2 ? lanechunk<2> : depth == 3 ? lanechunk<3> : lanechunk<1>;
+  CHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kThreads, lds));
+  const uint32_t C = getenv("PC_C") ? uint32_t(atoi(getenv("PC_C"))) : 32768u;
   double maxg = 0;
   for (int a = 1; a < argc; ++a) maxg = atof(argv[a]) > maxg ? atof(argv[a]) : maxg;
   if (argc < 2) maxg = 16;
@@ -105,7 +114,7 @@ int main(int argc, char** argv) {
           hipLaunchKernelGGL(coalesced, dim3(cus * 8), dim3(kThreads), 0, 0, reinterpret_cast<const uint4*>(d), n / 16,
                              out);
         else
-          hipLaunchKernelGGL(lanechunk, dim3(cus * occ), dim3(kThreads), lds, 0, d, n, C, next, out);
+          hipLaunchKernelGGL(kern, dim3(cus * occ), dim3(kThreads), lds, 0, d, n, C, next, out);
         CHK(hipEventRecord(e1, 0));
         CHK(hipEventSynchronize(e1));
         float ms = 0.f;
@@ -115,7 +124,7 @@ int main(int argc, char** argv) {
           best = ms < best ? ms : best;
         }
       }
-      printf("%-10s gib=%.1f occ=%d avg_ms=%.3f GB/s=%.0f frac=%.4f best_GB/s=%.0f\n", k ? "lanechunk" : "coalesced", g,
+      printf("%-10s C=%u depth=%d gib=%.1f occ=%d avg_ms=%.3f GB/s=%.0f frac=%.4f best_GB/s=%.0f\n", k ? "lanechunk" : "coalesced", C, depth, g,
              occ, sum / reps, n / (sum / reps * 1e-3) / 1e9, n / (sum / reps * 1e-3) / 8e12, n / (best * 1e-3) / 1e9);
       fflush(stdout);
     }
