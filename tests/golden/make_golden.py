@@ -23,8 +23,14 @@ present here and agrees with Go on that case:
   perl as ``\\p{Script=Name}`` (perl's bare ``\\p{Greek}`` means
   Script_Extensions).
 
-A vector with no applicable witness (Unicode case folding, invalid UTF-8,
-Go syntax errors, ...) is still written, marked ``"witnesses": []`` — parity
+* ``py-regex``: the ``regex`` module (a third-party engine, VERSION0 = simple
+  case folding like Go's ``(?i)``) on each piece decoded as Go decodes it, for
+  patterns it reads as Go does once Go's ASCII ``\\s \\d \\w \\b`` and
+  ``\\x{...}`` are spelled out (``_pyregex_pattern``): Unicode classes,
+  scripts, folding and invalid UTF-8 data (not a Unicode class under ``(?i)``:
+  Go widens it by FoldCategory / FoldScript, regex does not).
+
+A vector with no applicable witness (Go syntax errors, Unicode classes under (?i)) is still written, marked ``"witnesses": []`` — parity
 unpinned for that case.
 
 Run from the repo root after `make` (needs oracle/liboracle.so, and
@@ -141,6 +147,91 @@ def _perl_lines(pattern: bytes, data: bytes):
     return [int(x) for x in p.stdout.split()]
 
 
+# ``py-regex``: the third-party ``regex`` module (VERSION0: simple case
+# folding, as Go's (?i)) in str mode on each piece decoded as Go decodes it,
+# for patterns it reads as Go does once Go's ASCII-only Perl and POSIX classes
+# and \x{...} are spelled out; skipped: those Perl escapes inside a bracket
+# class, Unicode classes under (?i), Go syntax errors (a parse result, not a
+# match).
+_ASCII_ESC = {
+    "s": r"[\t\n\f\r ]", "S": r"[^\t\n\f\r ]", "d": r"[0-9]", "D": r"[^0-9]",
+    "w": r"[0-9A-Za-z_]", "W": r"[^0-9A-Za-z_]",
+    "b": r"(?:(?<=[0-9A-Za-z_])(?![0-9A-Za-z_])|(?<![0-9A-Za-z_])(?=[0-9A-Za-z_]))",
+    "B": r"(?:(?<=[0-9A-Za-z_])(?=[0-9A-Za-z_])|(?<![0-9A-Za-z_])(?![0-9A-Za-z_]))",
+    "z": r"\Z",
+}
+
+
+_POSIX = {"upper": "A-Z", "lower": "a-z", "digit": "0-9", "alpha": "A-Za-z", "alnum": "0-9A-Za-z",
+          "xdigit": "0-9A-Fa-f", "space": "\\t\\n\\v\\f\\r ", "blank": "\\t ", "word": "0-9A-Za-z_"}
+
+
+def _pyregex_pattern(pattern: bytes):
+    """Go pattern -> an equivalent pattern for the regex module, or None."""
+    try:
+        import regex  # noqa: F401
+        p = pattern.decode("utf-8")
+    except (ImportError, UnicodeDecodeError):
+        return None
+    if O.compile_status(pattern) != O.ORC_OK or "\\Q" in p:
+        return None
+    # Go's POSIX classes are ASCII (regex reads them as Unicode properties)
+    for name, rng in _POSIX.items():
+        p = p.replace("[:%s:]" % name, rng)
+    if "[:" in p:
+        return None
+    # Go folds a class under (?i) through unicode.FoldCategory / FoldScript
+    # ((?i)\p{Greek} also matches U+00B5 and U+0345); regex does not
+    if "(?i" in p and ("\\p" in p or "\\P" in p):
+        return None
+    out, i, in_class = [], 0, False
+    while i < len(p):
+        c = p[i]
+        if c == "\\" and i + 1 < len(p):
+            e = p[i + 1]
+            if e == "x" and i + 2 < len(p) and p[i + 2] == "{":
+                j = p.index("}", i + 3)
+                out.append("\\U%08x" % int(p[i + 3:j], 16))
+                i = j + 1
+                continue
+            if e in _ASCII_ESC:
+                if in_class:
+                    return None
+                out.append(_ASCII_ESC[e])
+            else:
+                out.append(p[i:i + 2])
+            i += 2
+            continue
+        if c == "[" and not in_class:
+            in_class = True
+            out.append(c)
+            i += 1
+            # a leading ']' (or '^]') is a literal
+            if p[i:i + 1] == "^":
+                out.append("^")
+                i += 1
+            if p[i:i + 1] == "]":
+                out.append("\\]")
+                i += 1
+            continue
+        if c == "]" and in_class:
+            in_class = False
+        out.append(c)
+        i += 1
+    return "".join(out)
+
+
+def _pyregex_lines(pattern: bytes, data: bytes):
+    import regex
+
+    rp = _pyregex_pattern(pattern)
+    try:
+        rx = regex.compile(rp, flags=regex.VERSION0)
+    except regex.error:
+        return None
+    return [i + 1 for i, line in enumerate(data.split(b"\n")) if rx.search(_go_decode(line))]
+
+
 _INPUTS = []
 
 
@@ -167,6 +258,11 @@ def vector(name: str, filename: str, pattern: bytes, data: bytes):
             want = [x for x in ln if not (x == last and (data.endswith(b"\n") or not data))]
             assert g == want, (name, "gnu-grep disagrees with the oracle", g[:10], want[:10])
             witnesses.append("gnu-grep")
+    if _pyregex_pattern(pattern) is not None:
+        g = _pyregex_lines(pattern, data)
+        if g is not None:
+            assert g == ln, (name, "py-regex disagrees with the oracle", g[:10], ln[:10])
+            witnesses.append("py-regex")
     if _perl_ok(pattern, data):
         g = _perl_lines(pattern, data)
         if g is not None:

@@ -7,8 +7,9 @@ application/grep.go:13-36 (1-based line numbers, byte starts and lengths of
 the matching lines), the keys grep.go:25 builds, the key-sorted Reduce output
 lines (map_reduce/worker.go:111-124,163-165) and the ihash partitions
 (worker.go:13-17). Vectors whose "witnesses" list is non-empty were checked,
-when generated, against Python `re` and/or GNU grep; the rest are parity
-unpinned (DESIGN.md).
+when generated, against Python `re`, GNU grep, perl's regex engine and/or the
+`regex` module (test_witnesses_still_agree re-runs the Python ones); the rest
+are parity unpinned.
 """
 import base64
 import json
@@ -44,9 +45,34 @@ def _eq(got, want, name):
 def test_golden_shape():
     assert len(VECTORS) > 400
     pinned = [v for v in VECTORS if v["witnesses"]]
-    assert len(pinned) > 300
+    assert len(pinned) > 550
     assert any(v["go_syntax_error"] for v in VECTORS)
     assert any(v["name"].startswith("synth-c3") and v["line_no"] for v in VECTORS)
+
+
+def test_witnesses_still_agree():
+    """The Python witnesses re-run on every vector they pinned: Python `re` per
+    strings.Split piece, and the `regex` module on Go-decoded pieces."""
+    import importlib.util
+    import re
+    import sys
+
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(HERE, "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    sys.modules.setdefault("make_golden", mg)
+    spec.loader.exec_module(mg)
+    n = {"python-re": 0, "py-regex": 0}
+    for v in VECTORS:
+        p, d = _unpack(v)
+        if "python-re" in v["witnesses"]:
+            rx = re.compile(p)
+            got = [i + 1 for i, line in enumerate(d.split(b"\n")) if rx.search(line)]
+            assert got == v["line_no"], v["name"]
+            n["python-re"] += 1
+        if "py-regex" in v["witnesses"]:
+            assert mg._pyregex_lines(p, d) == v["line_no"], v["name"]
+            n["py-regex"] += 1
+    assert n["python-re"] > 300 and n["py-regex"] > 500, n
 
 
 def test_oracle_reproduces_golden():
