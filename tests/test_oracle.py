@@ -6,6 +6,8 @@ tests or vectors, and no Go toolchain exists here):
 * Python `re` (bytes mode) on randomly generated patterns and lines restricted
   to the dialect subset where Go and Python agree (ASCII inputs, no `{,n}`,
   no `\\s`, no `(?i)`+non-ASCII);
+* the third-party `regex` module on Go-decoded pieces, for the Unicode
+  patterns `re` cannot read (categories, (?i) orbits, invalid UTF-8);
 * the SURVEY's ihash known answers and Go's JSON/Sprintf formats.
 """
 import random
@@ -153,3 +155,43 @@ def test_memoized_matcher_cache_flush():
         assert len(a[0]) > 10
         for x, y in zip(a, b):
             assert list(x) == list(y), pat
+
+
+def test_oracle_vs_regex_module_random():
+    """A second, third-party engine on the patterns Python `re` cannot read:
+    the `regex` module (VERSION0: simple case folding, like Go's (?i)) on each
+    strings.Split piece decoded as Go decodes it (an invalid byte is U+FFFD),
+    over random patterns from the compiler tests -- Unicode categories, (?i)
+    over the k/K/U+212A and s/S/U+017F orbits, \\b, anchors, \\x{FFFD},
+    repeats -- and random lines with invalid UTF-8. The pattern translation
+    (Go's ASCII \\s \\d \\w \\b and POSIX classes spelled out; skipped: Unicode
+    classes under (?i), where Go widens by FoldCategory) is the golden
+    generator's (tests/golden/make_golden.py)."""
+    import importlib.util
+    import os
+    import sys
+
+    pytest.importorskip("regex")
+    from test_compiler import ALPHA, _rand_pattern
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(here, "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    sys.modules.setdefault("make_golden", mg)
+    spec.loader.exec_module(mg)
+    rnd = random.Random(2718)
+    checked = patterns = 0
+    for _ in range(1500):
+        pat = _rand_pattern(rnd).encode()
+        if mg._pyregex_pattern(pat) is None:
+            continue
+        patterns += 1
+        for _ in range(6):
+            data = b"".join(rnd.choice(ALPHA) for _ in range(rnd.randint(0, 40)))
+            got = mg._pyregex_lines(pat, data)
+            if got is None:
+                break
+            want = [int(x) for x in O.grep_map(pat, data)[0]]
+            assert got == want, (pat, data)
+            checked += 1
+    assert patterns > 500 and checked > 3000, (patterns, checked)
