@@ -48,6 +48,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "scan_common.h"
 #include "../../../include/dgrep_blob.h"
@@ -1518,11 +1519,20 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
 // read from HBM (L2-resident: [state][class], u16 entries, or u32 above 65535
 // states). A line is read in aligned 16-byte pieces.
 constexpr uint32_t kVerifyHotBytes = 48 * 1024;
+constexpr uint32_t kVerifyLookback = 256;  // bytes a wave-verified segment's entry state is guessed from
 
 // The tile loop shared by both verification kernels: line_matches(a, e)
 // decides the candidate [a, e) (grep.go:21 on that line).
-template <class Pred>
-__device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_matches) {
+// Candidate lines longer than kVerifyWaveBytes are decided by the whole wave
+// (WavePred): one lane walking a 60 KiB line on the DFA held the kernel for
+// milliseconds (long-line workloads); see verify_kernel.
+constexpr uint64_t kVerifyWaveBytes = 16384;
+struct NoWavePred {
+  __device__ bool operator()(uint64_t, uint64_t) const { return false; }
+};
+template <class Pred, class WavePred = NoWavePred>
+__device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_matches, WavePred&& wave_matches = {}) {
+  constexpr bool kWave = !std::is_same<std::decay_t<WavePred>, NoWavePred>::value;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t waves = uint64_t(gridDim.x) * 4;
   for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
@@ -1532,7 +1542,7 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
     for (uint32_t k0 = 0; k0 < ti.count; k0 += 64) {
       const uint32_t k = k0 + lane;
       const uint64_t src = ti.base + k;
-      bool keep = false;
+      bool keep = false, wave = false;
       StagedLine L;
       if (k < ti.count && src < v.staging_cap) {
         L = v.staging[src];
@@ -1545,7 +1555,23 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
           L.meta = staged_rel(L) | (uint32_t(P.len >> 32) << 24);
         } else if (L.meta & kMetaCand) {
           L.meta &= ~kMetaCand;
-          keep = line_matches(L.start, L.start + staged_len(L));
+          if (kWave && staged_len(L) > kVerifyWaveBytes)
+            wave = true;
+          else
+            keep = line_matches(L.start, L.start + staged_len(L));
+        }
+      }
+      if constexpr (kWave) {
+        // the batch's long candidates, one at a time by all 64 lanes
+        const uint64_t len = wave ? staged_len(L) : 0u;
+        for (uint64_t wm = __ballot(wave); wm; wm &= wm - 1) {
+          const int j = __ffsll((unsigned long long)wm) - 1;
+          const uint64_t a = (uint64_t(uint32_t(__shfl(uint32_t(L.start >> 32), j, 64))) << 32) |
+                             uint32_t(__shfl(uint32_t(L.start), j, 64));
+          const uint64_t n = (uint64_t(uint32_t(__shfl(uint32_t(len >> 32), j, 64))) << 32) |
+                             uint32_t(__shfl(uint32_t(len), j, 64));
+          const bool r = wave_matches(a, a + n);
+          if (int(lane) == j) keep = r;
         }
       }
       const uint64_t m = __ballot(keep);
@@ -1575,14 +1601,38 @@ __global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
     const size_t i = size_t(s) * K + c;
     return i < hot_n ? uint32_t(hot[i]) : uint32_t(gfull[i]);
   };
-  verify_tiles(v, [&](uint64_t a, uint64_t e) {
-    uint32_t st = v.start;
+  // state after [a, e) from s, stopping at the absorbing MATCHED state
+  auto run = [&](uint64_t a, uint64_t e, uint32_t s) -> uint32_t {
+    if (s == v.matched) return s;
     for_line_bytes(v.data, a, e, [&](uint32_t b) {
-      st = next(st, cls[b]);
-      return st != v.matched;
+      s = next(s, cls[b]);
+      return s != v.matched;
     });
-    return next(st, cn) == v.start_m;
-  });
+    return s;
+  };
+  verify_tiles(
+      v, [&](uint64_t a, uint64_t e) { return next(run(a, e, v.start), cn) == v.start_m; },
+      [&](uint64_t a, uint64_t e) {
+        // a long candidate by the whole wave: lane j runs segment j from a
+        // GUESSED entry state (the state after the kVerifyLookback bytes
+        // before it, from start: exact for keyword automata such as config
+        // 4's); the lanes then compose in order from the true state, re-running
+        // (all lanes alike) a segment whose guess was wrong -- exact for any DFA
+        const uint64_t n = e - a, seg = (n + 63) / 64, lane = threadIdx.x & 63u;
+        const uint64_t sb = a + min(n, lane * seg), se = a + min(n, (lane + 1) * seg);
+        const uint64_t from = sb - min(sb - a, uint64_t(kVerifyLookback));
+        const uint32_t g = run(from, sb, v.start);
+        const uint32_t x = run(sb, se, g);
+        uint32_t s = v.start;
+        for (int j = 0; j < 64 && s != v.matched; ++j) {
+          const uint32_t gj = uint32_t(__shfl(g, j, 64)), xj = uint32_t(__shfl(x, j, 64));
+          if (gj == s)
+            s = xj;
+          else
+            s = run(a + min(n, uint64_t(j) * seg), a + min(n, uint64_t(j + 1) * seg), s);
+        }
+        return next(s, cn) == v.start_m || s == v.matched;
+      });
 }
 
 // ---- NFA verification (DGREP_DFA_PARTIAL) -----------------------------------

@@ -772,8 +772,13 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   HIPCHK(hipStreamSynchronize(c->stream));
   uint64_t total = 0;
   for (const PendingLine& p : P) total += p.end - p.line_start;
-  // about four segments per resident lane (two per lane per round), >= 16 KiB
-  const uint64_t seg = std::max<uint64_t>(uint64_t(16) << 10, (total / (uint64_t(c->num_cus) * 3072) + 15) & ~uint64_t(15));
+  // two segments per lane of ONE round of long_dfa_seg_kernel (one 1024-thread
+  // workgroup per CU): a second, partly filled round held half the CUs idle
+  // for a whole segment (long_c4: 384 workgroups over 256 CUs). Each line adds
+  // at most one partial segment, hence the npend in the divisor. >= 16 KiB.
+  const uint64_t lanes2 = uint64_t(c->num_cus) * 2048;
+  const uint64_t div = npend < lanes2 / 2 ? lanes2 - npend : uint64_t(c->num_cus) * 3072;
+  const uint64_t seg = std::max<uint64_t>(uint64_t(16) << 10, (total / div + 16) & ~uint64_t(15));
   std::vector<LongSeg> segs;
   std::vector<uint64_t> from, off(npend + 1, 0);
   const uint64_t lb = long_lookback();

@@ -455,6 +455,43 @@ def test_filter_candidates_dense_and_long(filter_ctx):
             assert st["stepper"] == "filter", st
 
 
+def test_filter_long_candidates_wave_verified(filter_ctx):
+    """Candidate lines above verify_kernel's wave threshold (16 KiB) are decided
+    by the whole wave from guessed segment entry states: keyword-style
+    patterns (the guess is exact), an anchored one and one whose state remembers
+    an unbounded past (guesses wrong, segments re-run in order), matches at the start, middle, end or not
+    at all, lines up to past the filter's park point; every line a candidate
+    (4 LDS rows) and the shipped LDS image."""
+    import dgrep
+
+    rnd = random.Random(1616)
+    alpha = [b"a", b"b", b"e", b"r", b"o", b"x", b"y", b"k", b" ", b"_", b"1", b"z"]
+    kws = dgrep.synth_keywords(4, 200)
+    lines = []
+    for i in range(40):
+        n = rnd.randrange(16500, 90000)
+        body = bytearray(b"".join(rnd.choice(alpha) for _ in range(n)))
+        where = rnd.choice(["none", "start", "mid", "end"])
+        tok = rnd.choice([b"error", b"ERROR abc", rnd.choice(kws).upper(), b"ab"])
+        if where == "start":
+            body[0:len(tok)] = tok
+        elif where == "mid":
+            m = rnd.randrange(len(body) - len(tok))
+            body[m:m + len(tok)] = tok
+        elif where == "end":
+            body[-len(tok):] = tok
+        lines.append(bytes(body))
+        lines.append(b"short line %d" % i)
+    data = b"\n".join(lines) + b"\n"
+    patterns = [b"error", b"(WARN|ERROR) [a-z_]+", b"^ab.*x", b"k[^z]*y",
+                b"(?i)(" + b"|".join(kws) + b")"]
+    for rows in (4, 0):
+        for pattern in patterns:
+            filter_ctx.set_stepper("filter", rows)
+            _check(filter_ctx, pattern, data, threads=16)
+            assert filter_ctx.scan_stats()["stepper"] == "filter"
+
+
 def test_filter_verification_with_overflow(filter_ctx):
     """Filter with 4 LDS rows (nearly every line a candidate) and lanes whose
     records overflow their slots + spill: candidates staged by the scan AND by
