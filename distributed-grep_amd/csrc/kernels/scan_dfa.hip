@@ -2307,12 +2307,14 @@ hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
 // of sending many lanes through the overflow pass (C4 at 16 KiB: 0.8 % of the
 // lanes overflow and the pass costs 8 % of the scan; at 8 KiB 0.07 %).
 constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
-// Per-stepper ceiling: the pair stepper peaks at 16 KiB on C3 (measured on
-// MI355X, nodefer: 8 KiB 4.43 ms, 16 KiB 4.39, 32 KiB 4.71 per 16 GiB): at
-// 32 KiB most of its ~40 records per lane and tile no longer fit the LDS slots
-// and go through the HBM spill area.
+// Per-stepper ceiling: the pair stepper stops at 8 KiB. Round 2 (static
+// tiles) measured 8 KiB 4.43 ms, 16 KiB 4.39, 32 KiB 4.71 per 16 GiB (at 32
+// KiB most of its ~40 records per lane and tile go through the HBM spill
+// area); with tiles claimed dynamically, 8 KiB was at least as fast as 16 KiB
+// on each of three boxes (+0.3 %, +2.5 %, and +7 % against a slow mode 16 KiB
+// fell into in 1 of 6 runs on the first; profiles/r04/ablation/c3_chunk*.txt).
 #ifndef DGREP_PAIR_MAX_CHUNK
-#define DGREP_PAIR_MAX_CHUNK 16384
+#define DGREP_PAIR_MAX_CHUNK 8192
 #endif
 // Doubling also stops below DGREP_MIN_TILES_X2 / 2 tiles per resident wave
 // (Sheng, pair; the filter keeps 1):
