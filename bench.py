@@ -110,6 +110,10 @@ def parse():
                     help="ablation: allocate at least this many GiB for the split's buffer")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the N-rank report (gloo, oracle instead of the GPU scan; value null)")
+    ap.add_argument("--exchange", choices=["auto", "capi", "torch"], default="auto",
+                    help="the N > 1 record gather inside each step: the C ABI's RCCL gather (capi, the default at "
+                         "N > 1) or dgrep/dist.py over torch.distributed (torch); capi at N = 1 rehearses the "
+                         "self-copy path and the gather check")
     ap.add_argument("--pattern", default=None,
                     help="ablation only: scan the workload's split with this pattern instead (not a BASELINE config)")
     return ap.parse_args()
@@ -205,6 +209,13 @@ def main():
                                                                  m["len"][:count], pattern, args.verify_windows,
                                                                  wl.get("verify_window", 2 << 20))}
 
+    # ---- the exchange: what rank 0 received in the last timed step ----------
+    gather = None
+    if world > 1 or m["comm"] is not None:
+        gather = check_gather(m, world, rank, dev, seed)
+        if m["comm"] is not None:
+            m["comm"].close()
+
     # ---- CPU comparators, on rank 0 while the other ranks wait ---------------
     cpu = cpu_mt = cpu_workers = None
     if world > 1:
@@ -223,7 +234,7 @@ def main():
     if world > 1:
         dist.barrier()
 
-    line = build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, cpu_mt, cpu_workers)
+    line = build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, cpu_mt, cpu_workers, gather)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -267,12 +278,22 @@ def measure_gpu(args, wl, world, rank, local, dev, n, pattern, seed):
         cap = int(cnt * 1.05) + 1024
     line_t, start_t, len_t = res
 
+    # N > 1: the path's only exchange -- compacted records -> rank 0 over
+    # RCCL/xGMI -- through the C ABI a Go worker binds (dgrep_gather_records_device,
+    # csrc/runtime/exchange.hip), on the scan's stream; checked after the timed
+    # steps against the torch path (check_gather)
     from dgrep.dist import gather_records
+
+    use_capi = args.exchange == "capi" or (args.exchange == "auto" and world > 1)
+    comm = open_comm(ctx, world, rank, dev) if use_capi else None
+    last = {}
 
     def step():
         c = ctx.scan_device(buf.data_ptr(), n, line_t.data_ptr(), start_t.data_ptr(), len_t.data_ptr(), cap)
-        if world > 1:
-            # the path's only exchange: compacted records -> rank 0 over RCCL/xGMI
+        if comm is not None:
+            last["gather"] = comm.gather_device(line_t.data_ptr(), start_t.data_ptr(), len_t.data_ptr(), c,
+                                                split=seed, root=0)
+        elif world > 1:
             gather_records(line_t, start_t, len_t, c, dst=0, split=seed)
         return c
 
@@ -293,7 +314,104 @@ def measure_gpu(args, wl, world, rank, local, dev, n, pattern, seed):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     return dict(buf=buf, line=line_t, start=start_t, len=len_t, count=count, kms=kms, stats=stats, elapsed=elapsed,
-                nstates=cp.nstates, nclasses=cp.nclasses, build=dgrep.build_info())
+                nstates=cp.nstates, nclasses=cp.nclasses, build=dgrep.build_info(), comm=comm,
+                gather=last.get("gather"), exchange="capi" if comm is not None else ("torch" if world > 1 else None))
+
+
+def open_comm(ctx, world, rank, dev):
+    """The C ABI's RCCL communicator (dgrep_comm_open) on the scan context's
+    device and stream: rank 0 makes the 128-byte id, torch.distributed hands it
+    to the others (a Go worker would use its own channel)."""
+    import torch
+    import torch.distributed as dist
+
+    import dgrep
+
+    if world == 1:  # --exchange capi at N = 1: the self-copy path (a rehearsal of the line's fields)
+        return dgrep.Comm(ctx, dgrep.Comm.unique_id(), 1, 0)
+    uid = torch.zeros(dgrep.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        uid.copy_(torch.frombuffer(bytearray(dgrep.Comm.unique_id()), dtype=torch.uint8))
+    dist.broadcast(uid, 0)
+    return dgrep.Comm(ctx, bytes(uid.cpu().numpy().tobytes()), world, rank)
+
+
+def record_checksum(line_t, start_t, len_t, count, split, dev):
+    """(count, split, sums of line / start / len, and a position-weighted sum
+    of all three) as int64 (sums wrap alike on every rank)."""
+    import torch
+
+    ln, st, le = (x[:count].to(torch.int64) for x in (line_t, start_t, len_t))
+    w = torch.arange(1, count + 1, dtype=torch.int64, device=ln.device)
+    v = [count, split, int(ln.sum()), int(st.sum()), int(le.sum()), int(((ln * 3 + st * 5 + le * 7) * w).sum())]
+    return torch.tensor(v, dtype=torch.int64, device=dev)
+
+
+def copy_device_records(ptr, total, dev):
+    """The comm-owned packed records (device pointer from
+    dgrep_gather_records_device) into a torch int32 tensor (hipMemcpy D2D)."""
+    import ctypes
+
+    import torch
+
+    from dgrep.dist import REC_WORDS
+
+    out = torch.empty(total * REC_WORDS, dtype=torch.int32, device=dev)
+    if total:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        rc = hip.hipMemcpy(out.data_ptr(), ptr, out.numel() * 4, 3)  # hipMemcpyDeviceToDevice
+        if rc != 0:
+            raise RuntimeError("hipMemcpy of the gathered records failed: %d" % rc)
+    return out
+
+
+def check_gather(m, world, rank, dev, seed):
+    """After the timed steps: the records rank 0 received in the LAST timed
+    step must be every rank's own records, in rank order, with its split id.
+    Checked two ways: per-rank checksums all-gathered from the ranks
+    themselves, and (C ABI exchange) record-by-record against the torch path
+    (dgrep/dist.py gather_records) run once more over the same arrays."""
+    import torch
+    import torch.distributed as dist
+
+    from dgrep.dist import gather_records, unpack_records
+
+    count = m["count"]
+    mine = record_checksum(m["line"], m["start"], m["len"], count, seed, dev)
+    if world > 1:
+        allc = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine)
+        ref = gather_records(m["line"], m["start"], m["len"], count, dst=0, split=seed)
+    else:
+        allc = [mine]
+        ref = [tuple(x[:count].to(torch.int64) for x in (m["line"], m["start"], m["len"])) +
+               (torch.full((count,), seed & 0xFFFFFFFF, dtype=torch.int64, device=dev),)]
+    if rank != 0:
+        return None
+    want = [c.cpu().tolist() for c in allc]
+    ok = True
+    for r, (ln, st, le, sp) in enumerate(ref):
+        got = record_checksum(ln, st, le, ln.numel(), want[r][1], dev).cpu().tolist()
+        ok = ok and got == want[r] and bool((sp == want[r][1]).all())
+    out = {"exchange": m["exchange"] or "torch", "records": sum(w[0] for w in want),
+           "per_rank_counts": [w[0] for w in want], "checksums_match": bool(ok)}
+    if m["exchange"] == "capi":
+        ptr, total, counts = m["gather"]
+        same = total == out["records"] and counts == out["per_rank_counts"]
+        if same:
+            packed = copy_device_records(ptr, total, dev)
+            off = 0
+            for r, (ln, st, le, sp) in enumerate(ref):
+                c = ln.numel()
+                g = unpack_records(packed[off * 7:(off + c) * 7], c)
+                same = same and all(torch.equal(a, b) for a, b in zip(g, (ln, st, le, sp)))
+                off += c
+        out["capi_equals_torch_path"] = bool(same)
+        ok = ok and same
+    out["gather_verified"] = bool(ok)
+    log("gather check: %s" % json.dumps(out))
+    return out
 
 
 def measure_dry(args, wl, world, rank, local, dev, n, pattern, seed):
@@ -325,6 +443,7 @@ def measure_dry(args, wl, world, rank, local, dev, n, pattern, seed):
         res = (torch.from_numpy(ln.astype(np.int64)), torch.from_numpy(st.astype(np.int64)),
                torch.from_numpy(le.astype(np.int64)))
         if world > 1:
+            # the CPU rehearsal exchanges over gloo with the torch path
             gather_records(res[0], res[1], res[2], count, dst=0, split=seed)
         stats.append(dict(stepper="oracle (dry run)", lane_chunk=0, overflow_ms=0.0, verify_ms=0.0,
                           scan_ms=kms[-1], candidates=0, overflow_lanes=0, pending=0))
@@ -332,10 +451,11 @@ def measure_dry(args, wl, world, rank, local, dev, n, pattern, seed):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     return dict(buf=buf, line=res[0], start=res[1], len=res[2], count=count, kms=kms, stats=stats, elapsed=elapsed,
-                nstates=0, nclasses=0, build=dgrep.build_info())
+                nstates=0, nclasses=0, build=dgrep.build_info(), comm=None, gather=None,
+                exchange="torch (gloo, dry run)")
 
 
-def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, cpu_mt, cpu_workers):
+def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, cpu_mt, cpu_workers, gather=None):
     """The JSON line (rank 0 prints it). Every rank takes part in the
     reductions: wall time = max over ranks; the roofline comes from the SLOWEST
     rank's kernel time (max over ranks of its mean), per GPU and for the node."""
@@ -439,6 +559,10 @@ def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, c
     }
     if world > 1:
         out["cpu_baseline_workers"] = cpu_workers
+    if gather is not None:
+        out["exchange"] = gather["exchange"] if gather else m["exchange"]
+        out["gather_verified"] = bool(gather and gather["gather_verified"])
+        out["gather"] = gather
     if args.dry_run:
         out["dry_run"] = ("CPU rehearsal (gloo): the split is scanned by the oracle, not by the GPU; "
                           "value is null and no number here measures this framework")

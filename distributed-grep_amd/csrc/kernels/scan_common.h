@@ -5,26 +5,29 @@
 namespace dgrep {
 
 // One matching line as produced by a tile, before global ordering.
-// meta = rel | flags | len_hi: `rel` (bits 0-21) = number of '\n' between the
+// meta = rel | flags | len_hi: `rel` (bits 0-22) = number of '\n' between the
 // tile start and the line start, so the 1-based line number
-// (application/grep.go:25 `line_number+1`) is newlines_before_tile + rel + 1
-// (a tile is at most 64 x 32 KiB, so rel < 2^21); bit 22 = filter CANDIDATE
-// (verified afterwards); bit 23 = PENDING long line (len_lo = its index in the
-// pending list, resolved afterwards); bits 24-31 = bits 32-39 of the length
-// (lines up to 1 TiB: more than HBM holds).
+// (application/grep.go:25 `line_number+1`) is newlines_before_tile + rel + 1.
+// A tile is at most 64 x 64 KiB = 2^22 bytes, and its last lane's last line
+// can start right after a tile made of nothing but '\n': rel <= 2^22 needs 23
+// bits (round 4 had 22, enough for 32 KiB chunks only). Bit 23 = filter
+// CANDIDATE (verified afterwards); bit 24 = PENDING long line (len_lo = its
+// index in the pending list, resolved afterwards); bits 25-31 = bits 32-38 of
+// the length (lines up to 512 GiB: more than the 288 GB of HBM hold).
 struct StagedLine {
   uint64_t start;  // absolute byte offset of the line in the split
   uint32_t len_lo; // bytes, '\n' excluded (low 32 bits)
   uint32_t meta;
 };
-constexpr uint32_t kRelBits = 22;
-constexpr uint32_t kMetaCand = 1u << 22;
-constexpr uint32_t kMetaPend = 1u << 23;
+constexpr uint32_t kRelBits = 23;
+constexpr uint32_t kMetaCand = 1u << 23;
+constexpr uint32_t kMetaPend = 1u << 24;
+constexpr uint32_t kLenHiShift = 25;
 __host__ __device__ inline uint32_t meta_of(uint32_t rel, uint64_t len, bool cand) {
-  return rel | (cand ? kMetaCand : 0u) | (uint32_t(len >> 32) << 24);
+  return rel | (cand ? kMetaCand : 0u) | (uint32_t(len >> 32) << kLenHiShift);
 }
 __host__ __device__ inline uint64_t staged_len(const StagedLine& L) {
-  return uint64_t(L.len_lo) | (uint64_t(L.meta >> 24) << 32);
+  return uint64_t(L.len_lo) | (uint64_t(L.meta >> kLenHiShift) << 32);
 }
 __host__ __device__ inline uint32_t staged_rel(const StagedLine& L) { return L.meta & ((1u << kRelBits) - 1u); }
 
@@ -199,9 +202,12 @@ struct VerifyArgs {
 
 // LDS slot records (8 B: start16 | rel16, then w1): w1 = the line's length with
 // bit 31 the filter CANDIDATE flag; a length of kSlotLong or more (only a
-// lane's LAST owned line can reach past its <= 32 KiB chunk) is stored as
+// lane's LAST owned line can reach past its <= 64 KiB chunk) is stored as
 // kSlotLong and the lane keeps the real length (or its pending index) in
-// LaneRun::tail.
+// its ScanArgs::tails entry. The same holds for a last line that starts
+// exactly AT the chunk end (its '\n' predecessor is the chunk's last byte):
+// start = C = 65,536 does not fit 16 bits, so it is flagged in the tail
+// (kTailAtEnd) and read back as start C, rel = the chunk's '\n' count.
 constexpr uint32_t kCandidateBit = 0x80000000u;
 constexpr uint32_t kSlotLong = 0x7fffffffu;
 
@@ -237,6 +243,17 @@ constexpr uint32_t kFilterClassBytes = 256;
 // (Byte-table swizzles and a u8 class table were measured slower on MI355X:
 // these steppers are VALU-issue-bound)
 constexpr uint32_t kPairMaxT2 = 32768;
+// DGREP_PAIR_U8 (off: measured neutral, C3 0.530 vs 0.531 same box, r05): the
+// byte tables are ONE u8 table C[b] = 2 * class(b)
+// at LDS address 0 instead of the u32 UA / UB tables. A u8 table keeps four
+// byte values per dword, so printable ASCII spans 24 dwords in 24 distinct
+// banks and a wave's class reads of text never conflict (u32 entries put 'a',
+// 'A' and '!' in one bank: 47 % of C3's LDS cycles were conflicts, r04); the
+// pair's column offset 2 (c1 K + c2) = C[b0] K + C[b1] costs one v_mad_u32_u24
+// per pair, off the dependent chain.
+#ifndef DGREP_PAIR_U8
+#define DGREP_PAIR_U8 0
+#endif
 constexpr uint32_t kPairMaxImage = 40960;
 constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the byte tables)
 

@@ -53,6 +53,17 @@
 #include "scan_common.h"
 #include "../../../include/dgrep_blob.h"
 
+// Build parts: the Makefile compiles this file once per DGREP_SCAN_PART -- 0:
+// the kernels that take no stepper (verification, long lines, ordering) and
+// the host glue; 1: Sheng; 2: pair; 3: table; 4: filter + wide -- so the
+// stepper instantiations compile in parallel. Without the macro one
+// translation unit holds everything (tools/build_commit_variant.sh).
+#ifdef DGREP_SCAN_PART
+#define DG_PART(k) (DGREP_SCAN_PART == (k))
+#else
+#define DG_PART(k) 1
+#endif
+
 // Build-time tuning knobs, per stepper (defaults are the shipped configuration,
 // measured on MI355X; DESIGN.md §3 lists the variants that lost and were removed):
 //   CHUNK    bytes per lane chunk (multiple of BLOCK; the adaptive steppers
@@ -281,7 +292,8 @@ struct StepWide {
 
 // DFA whose two-byte table fits in LDS (2 * S' * K^2 <= kPairMaxT2 bytes; C3's
 // 20-state, 12-class regex: 6 KiB): ONE table lookup per TWO input bytes.
-// LDS image (kPairT2 = 2 KiB of byte tables first, at LDS address 0):
+// LDS image (kPairT2 = 2 KiB of byte tables first, at LDS address 0; with
+// DGREP_PAIR_U8 one u8 table C[b] = 2 class(b) there instead, see scan_common.h):
 //   UA, UB (u32 [256] each): UA[b] = 2K*class(b), UB[b] = 2*class(b), so the
 //      pair's column offset 2*(c1*K + c2) = UA[b0] + UB[b1]; the four lookups
 //      of a word share one address (4*b, UB by the instruction's immediate
@@ -316,6 +328,12 @@ struct StepPair {
     return *reinterpret_cast<const uint32_t*>(lds + kBase + 1024u + 4u * b);
   }
   __device__ __forceinline__ Pre prep_bytes(uint32_t x) const {
+    if constexpr (DGREP_PAIR_U8) {
+      // C[b] = 2 class(b) (u8 at LDS 0): a0 = 2 (c0 K + c1), a2 = 2 (c2 K + c3)
+      const uint8_t* c8 = lds + kBase;
+      const uint32_t c0 = c8[x & 0xffu], c1 = c8[(x >> 8) & 0xffu], c2 = c8[(x >> 16) & 0xffu], c3 = c8[x >> 24];
+      return Pre{__umul24(c0, K) + c1, 0u, __umul24(c2, K) + c3, 0u};
+    }
     // byte 0's table offset 4 * b0 as ONE v_lshlrev_b32_sdwa (hipcc emits
     // v_lshlrev + v_and for byte 0 while bytes 1-3 get the SDWA form)
     uint32_t o0;
@@ -348,7 +366,8 @@ struct StepPair {
   }
   // single-byte step (rare paths): state id = (premultiplied state - T2 base) / row bytes
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-    return T1[((s - kT2) / div) * K + (ub(b) >> 1)];
+    const uint32_t c = DGREP_PAIR_U8 ? uint32_t(lds[kBase + b]) >> 1 : ub(b) >> 1;
+    return T1[((s - kT2) / div) * K + c];
   }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
   __device__ __forceinline__ bool any2(uint32_t s1, uint32_t s3) const { return max(s1, s3) >= thr; }
@@ -473,13 +492,19 @@ static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must
 static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>::C % Tune<StepTable>::B == 0,
               "chunk must be a multiple of the block");
 // the LDS slots pack a matching line's chunk-relative start and '\n' index in
-// 16 bits each (Emitter): no compiled or runtime chunk may exceed 32 KiB
-// (a 64 KiB build -- start < C and rel <= start still fit 16 bits -- failed the
-// 32 GiB C5 full-split parity in round 4 and was not pursued)
-constexpr int kMaxLaneChunk = 32768;
+// 16 bits each (Emitter): a start below 65,536 and rel <= start fit, and the
+// one start that does not -- a lane's last line starting exactly AT its chunk
+// end C = 65,536 -- is flagged in the lane's tail (kTailAtEnd). Round 4's 64 KiB
+// build packed that start as 0 and ORed bit 16 into rel, which failed the
+// 32 GiB C5 full-split parity.
+#ifndef DGREP_MAX_LANE_CHUNK
+#define DGREP_MAX_LANE_CHUNK 65536
+#endif
+constexpr int kMaxLaneChunk = DGREP_MAX_LANE_CHUNK;
+static_assert(kMaxLaneChunk <= 65536, "16-bit slot offsets and 23-bit tile-relative line indices");
 static_assert(Tune<StepSheng8>::C <= kMaxLaneChunk && Tune<StepTable>::C <= kMaxLaneChunk &&
                   Tune<StepWide>::C <= kMaxLaneChunk,
-              "lane chunk above 32 KiB overflows the 16-bit LDS slot offsets");
+              "lane chunk above 64 KiB overflows the 16-bit LDS slot offsets");
 
 // chunks per lane: the table stepper runs two in lockstep while its table is
 // small (<= 64 states); a bigger table would lose more occupancy (the LDS
@@ -500,8 +525,16 @@ struct LaneRun {
   uint32_t nev;      // matching lines emitted
 };
 // ScanArgs::tails entry of a lane whose last record's slot holds kSlotLong: the
-// real length, or (bit 63) a PENDING line's index in the pending list
+// real length, or (bit 63) a PENDING line's index in the pending list; bit 62
+// (either case): the line starts exactly at the chunk end, see kSlotLong
 constexpr uint64_t kTailPending = 1ull << 63;
+constexpr uint64_t kTailAtEnd = 1ull << 62;
+// slot word 0 of a line starting at chunk-relative `start` (<= C <= 64 KiB)
+// with `rel` '\n' of the chunk before it; a start of 65,536 (= C, the lane's
+// last line) is flagged in the tail instead (returns kTailAtEnd)
+__device__ __forceinline__ uint64_t slot_at_end(int64_t start) {
+  return uint64_t(start) > 0xffffu ? kTailAtEnd : 0u;
+}
 
 template <int E, bool DIRECT>
 struct Emitter {
@@ -539,14 +572,16 @@ struct Emitter {
         a->staging[o] = L;
       }
     } else {
-      // only the lane's last owned line can reach past its <= 32 KiB chunk
+      // only the lane's last owned line can reach past its <= 64 KiB chunk
+      // or start at its end
+      const uint64_t ae = slot_at_end(start);
       uint32_t lw = uint32_t(len) | (cand ? kCandidateBit : 0u);
-      if (len >= kSlotLong) {
+      if (len >= kSlotLong || ae) {
         lw = kSlotLong | (cand ? kCandidateBit : 0u);
-        *tail = len;
+        *tail = len | ae;
       }
-      // start < C and rel < C fit 16 bits each
-      const uint32_t w0 = uint32_t(start) | (rel << 16);
+      // start < 65,536 and rel <= start fit 16 bits each
+      const uint32_t w0 = ae ? 0u : uint32_t(start) | (rel << 16);
       if (r.nev < uint32_t(E)) {
         slots[r.nev * 2 + 0] = w0;
         slots[r.nev * 2 + 1] = lw;
@@ -562,8 +597,9 @@ struct Emitter {
   // slot mode: the lane's last owned line is left PENDING (pending-list index
   // idx), resolved after the scan (long_end / long_map / long_fin kernels)
   __device__ __forceinline__ void pending(LaneRun& r, int64_t start, uint32_t rel, uint64_t idx) const {
-    const uint32_t w0 = uint32_t(start) | (rel << 16);
-    *tail = kTailPending | idx;
+    const uint64_t ae = slot_at_end(start);
+    const uint32_t w0 = ae ? 0u : uint32_t(start) | (rel << 16);
+    *tail = kTailPending | ae | idx;
     if (r.nev < uint32_t(E)) {
       slots[r.nev * 2 + 0] = w0;
       slots[r.nev * 2 + 1] = kSlotLong;
@@ -584,7 +620,7 @@ struct Emitter {
     }
     ++r.nev;
   }
-  // The same for a line wholly inside the lane's chunk (start < q < C <= 32 KiB):
+  // The same for a line wholly inside the lane's chunk (start < q < C <= 64 KiB):
   // 32-bit chunk-relative positions, no length checks.
   // inner() for the slot mode with a dummy slot E (flat_emit()): own = the
   // lane owns the line. A write for a line it does not own lands in a slot (or
@@ -1422,17 +1458,22 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
             // index) the lane kept in its tails entry
             uint64_t len = w1 & kSlotLong;
             uint32_t flags = (w1 & kCandidateBit) ? kMetaCand : 0u;
+            uint32_t off = w0 & 0xffffu, rel = w0 >> 16;
             if (len == kSlotLong) {
               len = tails[k];
-              if (len & kTailPending) {
-                len &= ~kTailPending;
-                flags |= kMetaPend;
+              if (len & kTailAtEnd) {
+                // the line starts at the chunk end (C = 64 KiB does not fit
+                // the slot's 16 bits): every '\n' of the chunk lies before it
+                off = C;
+                rel = nlc[k];
               }
+              if (len & kTailPending) flags |= kMetaPend;
+              len &= ~(kTailPending | kTailAtEnd);
             }
             StagedLine L;
-            L.start = cs[k] + (w0 & 0xffffu);
+            L.start = cs[k] + off;
             L.len_lo = uint32_t(len);
-            L.meta = (nl_off[k] + (w0 >> 16)) | flags | (flags & kMetaPend ? 0u : uint32_t(len >> 32) << 24);
+            L.meta = (nl_off[k] + rel) | flags | (flags & kMetaPend ? 0u : uint32_t(len >> 32) << kLenHiShift);
             a.staging[o] = L;
           }
         }
@@ -1446,7 +1487,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
           ol.out_base = o0;
           ol.nl_prefix = nl_off[k];
           // a parked last line: its pending index + 1 (the pass stops there too)
-          ol.pend = r[k].parked ? uint32_t(tails[k] & ~kTailPending) + 1u : 0u;
+          ol.pend = r[k].parked ? uint32_t(tails[k] & ~(kTailPending | kTailAtEnd)) + 1u : 0u;
           a.overflow[q] = ol;
         }
       }
@@ -1508,6 +1549,7 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
   }
 }
 
+#if DG_PART(0)
 // ---- filter verification (kStepFilter) -------------------------------------
 // One wave per tile: every candidate line (kCandidateBit) of the tile's staged
 // lines is re-run from its start on the WHOLE DFA and kept iff the '\n' after
@@ -1552,7 +1594,7 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
           const PendingLine P = v.pend[L.len_lo];
           keep = P.matched != 0u;
           L.len_lo = uint32_t(P.len);
-          L.meta = staged_rel(L) | (uint32_t(P.len >> 32) << 24);
+          L.meta = staged_rel(L) | (uint32_t(P.len >> 32) << kLenHiShift);
         } else if (L.meta & kMetaCand) {
           L.meta &= ~kMetaCand;
           if (kWave && staged_len(L) > kVerifyWaveBytes)
@@ -2246,10 +2288,14 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
   }
 }
 
+#endif  // DG_PART(0)
+
 // ---- host-side launchers (called from dgrep_runtime.cpp) ----------------
 
+#if DG_PART(0)
 uint32_t scan_table_row() { return kRow; }
 uint32_t scan_max_lane_chunk() { return uint32_t(kMaxLaneChunk); }
+#endif
 
 namespace {
 template <class Step>
@@ -2276,31 +2322,14 @@ hipError_t occ_t(int* b) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, scan_dfa8_kernel<Step, TBL, NT>, NT, 0);
 }
 
-// One switch for every entry point: stepper by kind, LDS image by size.
-template <class Op>
-hipError_t dispatch(int kind, uint32_t table_bytes, Op op) {
-  if (kind == kStepSheng8) return op.template run<StepSheng8, 2048>();
-  if (kind == kStepPair) {
-    if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
-    if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB)
-    if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
-    return op.template run<StepPair, int(kPairMaxImage)>();
-  }
-  if (kind == kStepWide) return op.template run<StepWide, int(kWideClassBytes + kWideHotBytes)>();
-  if (kind == kStepFilter) return op.template run<StepFilter, int(kFilterImageBytes)>();
-  if (table_bytes <= 16 * kRow) return op.template run<StepTable, 16 * kRow>();
-  if (table_bytes <= 32 * kRow) return op.template run<StepTable, 32 * kRow>();
-  if (table_bytes <= 64 * kRow) return op.template run<StepTable, 64 * kRow>();
-  if (table_bytes <= 128 * kRow) return op.template run<StepTable, 128 * kRow>();
-  return op.template run<StepTable, 256 * kRow>();
-}
 // Adaptive chunk: a power of two from the compiled chunk (its floor) up to
 // kShengMaxChunk, the largest that still gives every resident wave at least
 // one tile. Measured on C2 (profiles/r01/ablation/chunk_sweep.txt): 32 KiB
 // runs 5.1 TB/s, 16 KiB 4.74-4.88, 8 KiB 4.54, 4 KiB 4.29, but 14,592 B (a
 // chunk sized to fill whole rounds exactly) 4.13: keep powers of two. The LDS
 // slots pack a line's chunk-relative start (<= C) and '\n' index (<= C) in 16
-// bits each, so 32,768 is also the hard limit (65,536 fails GPU parity).
+// bits each, with a start of exactly C = 65,536 flagged in the lane's tail:
+// 64 KiB is the hard limit, reached by Sheng splits of >= 30 GiB (C5).
 // `dens_cap` (0 = none) is the largest chunk whose expected matching lines,
 // at the match density of the previous scan of this pattern, fill at most a
 // quarter of a lane's LDS slots: a denser pattern keeps smaller chunks instead
@@ -2322,6 +2351,11 @@ constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
 // slower than 4 tiles of half the chunk (12 GiB: 32 KiB 4,462-4,580 GB/s,
 // 16 KiB 5,152), while 2.67 (16 GiB) and 5.33 (32 GiB) tiles per wave at
 // 32 KiB beat 16 KiB (profiles/r04/ablation/chunk_dyn.txt).
+// The filter stops at 32 KiB (64 KiB chunks were measured on the Sheng
+// stepper's access pattern only).
+#ifndef DGREP_FILTER_MAX_CHUNK
+#define DGREP_FILTER_MAX_CHUNK 32768
+#endif
 #ifndef DGREP_MIN_TILES_X2
 #define DGREP_MIN_TILES_X2 5
 #endif
@@ -2333,6 +2367,10 @@ uint32_t adaptive_chunk_bytes(uint64_t n, uint64_t waves, uint64_t floor_c, uint
     c *= 2;
   return uint32_t(c);
 }
+}  // namespace
+
+// The stepper entry points (one per op), instantiated by their build part.
+namespace scan_ops {
 struct TileOp {
   uint64_t* bytes;
   uint32_t* chunk;
@@ -2356,7 +2394,9 @@ struct TileOp {
     if constexpr (adaptive_chunk<S, T>())
       c = force ? uint64_t(force)
                 : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap,
-                                       S::kKind == kStepPair ? DGREP_PAIR_MAX_CHUNK : kShengMaxChunk,
+                                       S::kKind == kStepPair     ? DGREP_PAIR_MAX_CHUNK
+                                       : S::kKind == kStepFilter ? DGREP_FILTER_MAX_CHUNK
+                                                                 : kShengMaxChunk,
                                        // the filter keeps 32 KiB at 2 tiles per wave (C4: 16 KiB -1.5 %)
                                        S::kKind == kStepFilter ? 2 : DGREP_MIN_TILES_X2);
     *chunk = uint32_t(c);
@@ -2384,7 +2424,72 @@ struct OverflowOp {
   template <class S, int T>
   hipError_t run() const { return overflow_t<S, T>(*a, n, s); }
 };
-}  // namespace
+
+// stepper by kind, LDS image by size; one function per build part
+template <class Op>
+hipError_t part_sheng(int, uint32_t, const Op& op) {
+  return op.template run<StepSheng8, 2048>();
+}
+template <class Op>
+hipError_t part_pair(int, uint32_t table_bytes, const Op& op) {
+  if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
+  if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB)
+  if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
+  return op.template run<StepPair, int(kPairMaxImage)>();
+}
+template <class Op>
+hipError_t part_table(int, uint32_t table_bytes, const Op& op) {
+  if (table_bytes <= 16 * kRow) return op.template run<StepTable, 16 * kRow>();
+  if (table_bytes <= 32 * kRow) return op.template run<StepTable, 32 * kRow>();
+  if (table_bytes <= 64 * kRow) return op.template run<StepTable, 64 * kRow>();
+  if (table_bytes <= 128 * kRow) return op.template run<StepTable, 128 * kRow>();
+  return op.template run<StepTable, 256 * kRow>();
+}
+template <class Op>
+hipError_t part_big(int kind, uint32_t, const Op& op) {
+  if (kind == kStepWide) return op.template run<StepWide, int(kWideClassBytes + kWideHotBytes)>();
+  return op.template run<StepFilter, int(kFilterImageBytes)>();
+}
+// explicit instantiations in their part, extern elsewhere
+#define DG_OPS(PFX, FN)                                                   \
+  PFX hipError_t FN<TileOp>(int, uint32_t, const TileOp&);                \
+  PFX hipError_t FN<OccOp>(int, uint32_t, const OccOp&);                  \
+  PFX hipError_t FN<LaunchOp>(int, uint32_t, const LaunchOp&);            \
+  PFX hipError_t FN<OverflowOp>(int, uint32_t, const OverflowOp&);
+#if DG_PART(1)
+DG_OPS(template, part_sheng)
+#else
+DG_OPS(extern template, part_sheng)
+#endif
+#if DG_PART(2)
+DG_OPS(template, part_pair)
+#else
+DG_OPS(extern template, part_pair)
+#endif
+#if DG_PART(3)
+DG_OPS(template, part_table)
+#else
+DG_OPS(extern template, part_table)
+#endif
+#if DG_PART(4)
+DG_OPS(template, part_big)
+#else
+DG_OPS(extern template, part_big)
+#endif
+#undef DG_OPS
+
+// One switch for every entry point: stepper by kind.
+template <class Op>
+hipError_t dispatch(int kind, uint32_t table_bytes, const Op& op) {
+  if (kind == kStepSheng8) return part_sheng(kind, table_bytes, op);
+  if (kind == kStepPair) return part_pair(kind, table_bytes, op);
+  if (kind == kStepWide || kind == kStepFilter) return part_big(kind, table_bytes, op);
+  return part_table(kind, table_bytes, op);
+}
+}  // namespace scan_ops
+
+#if DG_PART(0)
+using namespace scan_ops;
 
 uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t resident_blocks, uint32_t force,
                          double density, uint32_t spill_per_lane, uint32_t* chunk, uint32_t* waves_per_block,
@@ -2487,5 +2592,7 @@ hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t s
     hipLaunchKernelGGL(verify_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, v);
   return hipGetLastError();
 }
+
+#endif  // DG_PART(0)
 
 }  // namespace dgrep

@@ -138,7 +138,11 @@ DG_HD void line(uint64_t seed, uint64_t page, uint32_t li, int kind, char* o, ui
 DG_HD void filler_page(uint64_t seed, uint64_t page, char* o, uint32_t bytes, bool kw = false) {
   Rng r{mix(seed + 0xf111) ^ mix(page)};
   const bool plant = r.below(2048) == 0;
-  const uint32_t at = r.below(bytes > 16 ? bytes - 16 : 1);
+  // a keyword (kind 4) is up to 12 bytes: planted 16 bytes before the page end;
+  // 'error' 8 before (kinds 2 / 3 as in round 3; round 4's long / long1g lines
+  // used the 16-byte placement for them too)
+  const uint32_t back = kw ? 16u : 8u;
+  const uint32_t at = r.below(bytes > back ? bytes - back : 1);
   uint32_t p = 0;
   while (p < bytes) {
     int wl;

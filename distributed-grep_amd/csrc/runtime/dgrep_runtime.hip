@@ -296,6 +296,11 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
     ua[b] = 2u * K * c;
     ub[b] = 2u * c;
   }
+  if (DGREP_PAIR_U8) {
+    // one u8 table C[b] = 2 class(b) at LDS 0 (over UA); 2 (K - 1) < 256
+    if (2u * (K - 1u) > 255u) return false;
+    for (int b = 0; b < 256; ++b) img->data()[b] = uint8_t(2u * h.byte_class[b]);
+  }
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
   *orig_out = orig;  // pair state index -> blob state (a shadow -> the state it copies)
@@ -942,7 +947,13 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   // Anything else shows in the counters, and the ordering is queued again once
   // the extra passes have run.
   const bool speculate = !filt && capacity != 0;
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  // Each buffer a scan can outgrow (overflow list, pending list, the filter's
+  // staging) is grown to what the scan counted and the scan re-run, so every
+  // grow is followed by a scan that fits: at most three grows, four scans. (A
+  // loop that could end on a grow left the filter's candidates unverified but
+  // counted.)
+  bool settled = false;
+  for (int attempt = 0; attempt < 4 && !settled; ++attempt) {
     a.staging = c->d_staging;
     a.capacity = c->staging_cap;
     a.overflow = c->d_overflow;
@@ -972,8 +983,12 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
       // candidates included, more staged lines than the staging buffer holds
       if ((rc = grow(c, &c->d_staging, &c->staging_cap, ctr[0] + ctr[0] / 8)) != DGREP_OK) return rc;
     } else {
-      break;
+      settled = true;
     }
+  }
+  if (!settled) {
+    c->err = "scan buffers still too small after three grows";
+    return DGREP_E_HIP;
   }
   const uint64_t staged = ctr[0];
   const uint64_t npend = park ? ctr[2] : 0;

@@ -153,8 +153,13 @@ extern "C" int dgrep_gather_records_device(dgrep_comm* m, const uint64_t* d_line
     HIPC(hipGetLastError());
   }
   if (m->rank != root) {
-    // 3. send (the root posts the matching receive in the same grouped call)
-    if (count) NCCLC(ncclSend(m->d_pack, count * kRecWords, ncclUint32, root, m->nccl, s));
+    // 3. send, grouped like the root's receives (and like the torch path,
+    // dgrep/dist.py: batch_isend_irecv on both sides)
+    if (count) {
+      NCCLC(ncclGroupStart());
+      NCCLC(ncclSend(m->d_pack, count * kRecWords, ncclUint32, root, m->nccl, s));
+      NCCLC(ncclGroupEnd());
+    }
     HIPC(hipStreamSynchronize(s));
     *total = count;
     return DGREP_OK;

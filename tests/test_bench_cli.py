@@ -58,3 +58,7 @@ def test_dry_run_world2_line():
     w = d["cpu_baseline_workers"]
     assert w and w["cores"] == 2 and w["workers"] == 2 and w["value"] > 0
     assert len(d["config"]["matching_lines_per_split"]) == 2
+    # the exchange: rank 0's gathered records checked against every rank's own
+    assert d["exchange"].startswith("torch") and d["gather_verified"] is True
+    g = d["gather"]
+    assert g["per_rank_counts"] == d["config"]["matching_lines_per_split"] and g["checksums_match"]

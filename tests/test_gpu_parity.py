@@ -107,7 +107,7 @@ def test_tile_and_chunk_boundaries(gpu_ctx, size):
 # splits (dgrep_set_lane_chunk forces them at oracle-friendly sizes): chunk and
 # tile edges, lines longer than a chunk, and more matching lines per lane than
 # LDS slots (pattern "" matches every line: the overflow kernel)
-@pytest.mark.parametrize("chunk", [4224, 8192, 14592, 16384, 32768])
+@pytest.mark.parametrize("chunk", [4224, 8192, 14592, 16384, 32768, 65536])
 def test_sheng_adaptive_chunks(gpu_ctx, chunk):
     import dgrep
 
@@ -134,10 +134,52 @@ def test_sheng_adaptive_chunks(gpu_ctx, chunk):
 def test_lane_chunk_validation(gpu_ctx):
     import dgrep
 
-    for bad in (100, 4000, 4097, 32896, 65536, 1 << 20):
+    for bad in (100, 4000, 4097, 32900, 65664, 131072, 1 << 20):
         with pytest.raises(dgrep.DgrepError):
             gpu_ctx.set_lane_chunk(bad)
     gpu_ctx.set_lane_chunk(0)
+
+
+@pytest.mark.parametrize("stepper", ["auto", "pair", "filter"])
+@pytest.mark.parametrize("chunk", [32768, 65536])
+def test_lines_starting_at_chunk_end(gpu_ctx, stepper, chunk):
+    """A lane's last owned line can start exactly AT its chunk end (the chunk's
+    last byte is '\\n'): at 64 KiB chunks that start (65,536) does not fit the
+    LDS slot's 16 bits -- round 4's 64 KiB build stored it as 0 and failed the
+    32 GiB C5 parity. Short and parked (pending) lines there, on every lane of
+    a tile; and a tile of nothing but '\\n' before a matching line, whose
+    tile-relative line index (64 C newlines = 2^22 at 64 KiB) needs 23 bits."""
+    import dgrep
+
+    tile = 64 * chunk
+    rnd = random.Random(chunk + len(stepper))
+    data = bytearray(dgrep.synth_corpus_host(3 * tile + 999, 21, 0))
+    for lane in range(3 * 64):
+        e = (lane + 1) * chunk - 1
+        data[e] = 0x0A
+        kind = rnd.randrange(4)
+        if kind == 0:  # a short matching line right at the chunk end
+            data[e + 1:e + 12] = b"error here\n"
+        elif kind == 1 and lane % 7 == 0:  # a long line from the chunk end (parked), matching at its far end
+            L = chunk + 4096 + 700 if rnd.random() < 0.5 else 2 * chunk + 300
+            L = min(L, len(data) - e - 40)
+            data[e + 1:e + 1 + L] = b"y" * (L - 8) + b"error!!\n"
+    data = bytes(data)
+    newline_tile = b"\n" * tile + b"x error\n" + b"ok\n" * 100 + b"\n" * (chunk - 1) + b"error tail"
+    try:
+        gpu_ctx.set_stepper(stepper)
+        gpu_ctx.set_lane_chunk(chunk)
+        for pattern in (b"error", b"^$|error", b"!!$", b"x error"):
+            cp = gpu_ctx.load(pattern)
+            _check(gpu_ctx, cp, data, threads=16)
+            st = gpu_ctx.scan_stats()
+            assert st["lane_chunk"] == chunk, st
+            # auto: Sheng for <= 8 states ("error"), else the pair stepper
+            assert st["stepper"] == stepper or (stepper == "auto" and st["stepper"] in ("sheng", "pair")), st
+            _check(gpu_ctx, cp, newline_tile, threads=16)
+    finally:
+        gpu_ctx.set_lane_chunk(0)
+        gpu_ctx.set_stepper("auto")
 
 
 # table-stepper instantiations: <= 64 states run two chunks per lane (tile 256
@@ -196,7 +238,7 @@ def _dense_lines(seed, count, maxlen):
     return b"\n".join(b"error WARN ab " + b"x" * rnd.randrange(maxlen) for _ in range(count))
 
 
-@pytest.mark.parametrize("chunk", [4096, 8192, 32768])
+@pytest.mark.parametrize("chunk", [4096, 8192, 32768, 65536])
 def test_overflow_pass_dense_every_chunk(gpu_ctx, chunk):
     """More matching lines per lane chunk than LDS slots at every Sheng chunk
     shipped: the wave-parallel overflow pass (one wave per lane chunk, 64
@@ -483,13 +525,32 @@ def test_filter_long_candidates_wave_verified(filter_ctx):
         lines.append(bytes(body))
         lines.append(b"short line %d" % i)
     data = b"\n".join(lines) + b"\n"
+    # only lines of 16.5-30 KiB: at 32 KiB chunks none is parked (a lane parks
+    # at 2 C), so every dropped candidate went through the wave verifier
+    mid = b"\n".join(l for l in lines if 16500 <= len(l) < 30000) + b"\n"
     patterns = [b"error", b"(WARN|ERROR) [a-z_]+", b"^ab.*x", b"k[^z]*y",
                 b"(?i)(" + b"|".join(kws) + b")"]
-    for rows in (4, 0):
-        for pattern in patterns:
-            filter_ctx.set_stepper("filter", rows)
-            _check(filter_ctx, pattern, data, threads=16)
-            assert filter_ctx.scan_stats()["stepper"] == "filter"
+    try:
+        # 32 KiB chunks: lines of 16-64 KiB stay candidates (wave-verified),
+        # longer ones are parked; 0 = adaptive (4 KiB here): lines over 8 KiB parked
+        for chunk in (32768, 0):
+            filter_ctx.set_lane_chunk(chunk)
+            for rows in (4, 0):
+                for pattern in patterns:
+                    filter_ctx.set_stepper("filter", rows)
+                    _check(filter_ctx, pattern, data, threads=16)
+                    st = filter_ctx.scan_stats()
+                    assert st["stepper"] == "filter"
+                    assert st["pending"] > 0, st
+                    if chunk and rows == 4:
+                        _check(filter_ctx, pattern, mid, threads=16)
+                        st = filter_ctx.scan_stats()
+                        assert st["pending"] == 0 and st["lane_chunk"] == chunk, st
+                        # 4 LDS rows: every line is a candidate; those not matching are dropped
+                        if pattern in (b"error", b"(WARN|ERROR) [a-z_]+", b"^ab.*x"):
+                            assert st["candidates"] > 0, st
+    finally:
+        filter_ctx.set_lane_chunk(0)
 
 
 def test_filter_verification_with_overflow(filter_ctx):
@@ -545,7 +606,7 @@ def test_pair_stepper_edges_and_random(pair_ctx, pattern):
         _check(gpu_ctx, cp, b"".join(rnd.choice(alpha) for _ in range(n // 3)))
 
 
-@pytest.mark.parametrize("chunk", [4096, 8192, 32768])
+@pytest.mark.parametrize("chunk", [4096, 8192, 32768, 65536])
 def test_pair_stepper_chunk_and_tile_edges(pair_ctx, chunk):
     import dgrep
 

@@ -18,13 +18,20 @@ for spec in "$@"; do
   defs=${spec#*=}
   (
     # the runtime builds the LDS images, so it takes the same knobs
-    $HIPCC $FLAGS $defs -c "$P/csrc/kernels/scan_dfa.hip" -o "$P/build/scan_dfa_$name.o" 2> "$P/build/variant_$name.log" &&
-      $HIPCC $FLAGS $defs -c "$P/csrc/runtime/dgrep_runtime.hip" -o "$P/build/dgrep_runtime_$name.o" 2>> "$P/build/variant_$name.log" &&
+    # the scan kernels' build parts in parallel (see scan_dfa.hip), then the runtime
+    pp=()
+    for k in 0 1 2 3 4; do
+      $HIPCC $FLAGS $defs -DDGREP_SCAN_PART=$k -c "$P/csrc/kernels/scan_dfa.hip" -o "$P/build/scan_dfa_${name}_p$k.o" 2> "$P/build/variant_${name}_p$k.log" &
+      pp+=($!)
+    done
+    $HIPCC $FLAGS $defs -c "$P/csrc/runtime/dgrep_runtime.hip" -o "$P/build/dgrep_runtime_$name.o" 2> "$P/build/variant_$name.log"
+    for q in "${pp[@]}"; do wait "$q"; done
+    ls "$P"/build/scan_dfa_${name}_p{0,1,2,3,4}.o > /dev/null &&
       mkdir -p "$P/build/stamp_$name" &&
       sed "s|#define DGREP_BUILD_FLAGS \".*\"|#define DGREP_BUILD_FLAGS \"$defs\"|" "$P/build/build_stamp.h" > "$P/build/stamp_$name/build_stamp.h" &&
       g++ -O2 -std=c++17 -fPIC -I"$P/build/stamp_$name" -c "$P/csrc/runtime/build_info.cpp" -o "$P/build/build_info_$name.o" &&
       $HIPCC -shared -fPIC --offload-arch=gfx950 -o "$P/variants/libdgrep_$name.so" \
-        "$P"/build/go_parser.o "$P"/build/dfa_builder.o "$P"/build/compile_api.o "$P/build/scan_dfa_$name.o" \
+        "$P"/build/go_parser.o "$P"/build/dfa_builder.o "$P"/build/compile_api.o "$P"/build/scan_dfa_${name}_p{0,1,2,3,4}.o \
         "$P"/build/encode.o "$P"/build/reduce.o "$P/build/dgrep_runtime_$name.o" "$P"/build/exchange.o "$P/build/build_info_$name.o" \
         -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &&
       echo "built $name ($defs)"
