@@ -31,6 +31,18 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 STAGED_LINE_BYTES = 16  # StagedLine written by the scan kernel per match
+FINAL_LINE_BYTES = 24   # the ABI's (u64 line_no, u64 start, u64 len) per match, when the scan places them itself
+
+
+def kernels_timed(stepper, in_scan):
+    """The kernels dgrep_last_kernel_ms covers for this stepper (roofline.kernel)."""
+    step = {"sheng": "StepSheng8", "pair": "StepPair", "table": "StepTable", "filter": "StepFilter",
+            "wide": "StepWide"}.get(stepper, str(stepper))
+    ks = ["dgrep::scan_dfa8_kernel<dgrep::%s>%s" % (step, " (in-scan ordering)" if in_scan else "")]
+    if stepper == "filter":
+        ks.append("dgrep::verify_kernel (candidate lines on the whole DFA)")
+    ks.append("dgrep::scan_overflow_kernel / long-line kernels when a scan needs them")
+    return ks
 LEN_DTYPE = "int64"  # torch dtype of the length array dgrep_scan_device writes (uint64 in dgrep.h)
 
 WORKLOADS = {
@@ -464,7 +476,12 @@ def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, c
     import torch.distributed as dist
 
     count, kms, stats = m["count"], m["kms"], m["stats"]
-    alg = n + STAGED_LINE_BYTES * count
+    # algorithmic bytes of the timed kernels: the split read once, plus per
+    # matching line the record the kernel leaves -- the ABI's final 24-byte
+    # record when it placed the lines itself (in-scan ordering), else the
+    # 16-byte staged record the ordering passes (not timed) read back
+    in_scan = bool(stats[-1].get("order_in_scan", 0))
+    alg = n + (FINAL_LINE_BYTES if in_scan else STAGED_LINE_BYTES) * count
     kern_ms, kern_med = float(np.mean(kms)), float(np.median(kms))
     mine = torch.tensor([m["elapsed"], kern_ms, kern_med, float(alg), float(count)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -529,7 +546,9 @@ def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, c
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "dgrep::scan_dfa8_kernel",
+            "kernel": kernels_timed(st["stepper"], in_scan)[0],
+            "kernels_timed": kernels_timed(st["stepper"], in_scan),
+            "record_bytes": FINAL_LINE_BYTES if in_scan else STAGED_LINE_BYTES,
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

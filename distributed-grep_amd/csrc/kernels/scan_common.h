@@ -125,8 +125,20 @@ struct ScanArgs {
   unsigned long long* pend_count;
   // Sheng stepper: the chunk maps instead of chunk_nl (nullptr: none)
   ChunkMap* chunk_map;
-  // tiles claimed after each wave's first (zeroed per launch)
+  // tiles claimed after each wave's first (zeroed per launch); with in-scan
+  // ordering, every tile
   unsigned long long* tile_next;
+  // in-scan ordering (out_line != nullptr; scan_dfa.hip order_tile): the final
+  // SoA output (capacity out_cap) and, per tile, the published aggregate and
+  // inclusive prefixes tagged with this launch's epoch (!= 0)
+  uint64_t* out_line;
+  uint64_t* out_start;
+  uint64_t* out_len;
+  uint64_t out_cap;
+  uint64_t* agg;
+  uint64_t* incl_c;
+  uint64_t* incl_l;
+  uint32_t epoch;
 };
 
 // the long-line kernels' arguments (long_end / long_map / long_fin)

@@ -928,9 +928,69 @@ __device__ __forceinline__ void run_block2(const Step& st, uint32_t M, const uin
   blk_finish(bb, sb, rb);
 }
 
+// Steppers whose dependent chain is LDS reads (pair: two per word, filter:
+// four): the NEXT word's first chain read is issued as soon as this word's
+// last state is known -- before this word's event test, event path and
+// newline bookkeeping, which then run under that read's latency instead of
+// in front of it (run_block_pipe). Bit k = stepper kind k.
+#ifndef DGREP_PIPE_KINDS
+#define DGREP_PIPE_KINDS ((1 << kStepPair) | (1 << kStepFilter))
+#endif
+template <class Step>
+constexpr bool pipe_chain() {
+  return ((DGREP_PIPE_KINDS) >> Step::kKind) & 1;
+}
+
+template <int BK, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void run_block_pipe(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
+                                               uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
+  Blk b;
+  blk_init<sentinel<Step>()>(b, pos, C, r);
+  constexpr int NW = BK / 4;
+  uint32_t w[NW];
+#pragma unroll
+  for (int i = 0; i < BK / 16; ++i) {
+    w[4 * i + 0] = v[i].x;
+    w[4 * i + 1] = v[i].y;
+    w[4 * i + 2] = v[i].z;
+    w[4 * i + 3] = v[i].w;
+  }
+  // pa: word J's state-independent lookups, pb: word J + 1's; f: word J's
+  // first chain read, in flight
+  typename Step::Pre pa = st.prep(w[0]);
+  uint32_t f = st.first(pa, r.s);
+  typename Step::Pre pb = st.prep(w[1]);
+  uint32_t s = r.s;
+#define DG_WP(J)                                                                          \
+  if ((J) < NW) {                                                                         \
+    /* filter: keep each word's work in place (as word_step does) */                     \
+    if (Step::kKind != kStepPair) __builtin_amdgcn_sched_barrier(0);                      \
+    uint32_t s0, s1, s2, s3;                                                              \
+    st.rest(pa, f, s0, s1, s2, s3);                                                       \
+    if ((J) + 1 < NW) {                                                                   \
+      f = st.first(pb, s3); /* issued before this word's events */                       \
+      pa = pb;                                                                            \
+      if ((J) + 2 < NW) pb = st.prep(w[(J) + 2 < NW ? (J) + 2 : 0]);                     \
+    }                                                                                     \
+    const uint32_t m = nl_mask(w[(J) < NW ? (J) : 0]);                                    \
+    word_events<J>(st, M, m, s0, s1, s2, s3, b, r, emit);                                 \
+    s = s3;                                                                               \
+  }
+  DG_WP(0) DG_WP(1) DG_WP(2) DG_WP(3) DG_WP(4) DG_WP(5) DG_WP(6) DG_WP(7)
+  DG_WP(8) DG_WP(9) DG_WP(10) DG_WP(11) DG_WP(12) DG_WP(13) DG_WP(14) DG_WP(15)
+  DG_WP(16) DG_WP(17) DG_WP(18) DG_WP(19) DG_WP(20) DG_WP(21) DG_WP(22) DG_WP(23)
+  DG_WP(24) DG_WP(25) DG_WP(26) DG_WP(27) DG_WP(28) DG_WP(29) DG_WP(30) DG_WP(31)
+#undef DG_WP
+  blk_finish(b, s, r);
+}
+
 template <int BK, bool MAP, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
+  if constexpr (!MAP && pipe_chain<Step>() && (Step::kKind == kStepPair || Step::kKind == kStepFilter)) {
+    run_block_pipe<BK>(st, M, v, pos, C, r, emit);
+    return;
+  }
   Blk b;
   blk_init<sentinel<Step>()>(b, pos, C, r);
   uint32_t s = r.s;
@@ -1322,12 +1382,148 @@ constexpr int waves_per_simd() {
 #ifndef DGREP_DYNAMIC_TILES
 #define DGREP_DYNAMIC_TILES 1
 #endif
-__device__ __forceinline__ uint64_t next_tile(const ScanArgs& a, uint64_t t, uint64_t waves) {
-  if (!DGREP_DYNAMIC_TILES) return t + waves;
+__device__ __forceinline__ uint64_t wave_sum_u64_(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t claim_tile(const ScanArgs& a) {
   uint64_t c = 0;
   if ((threadIdx.x & 63u) == 0) c = atomicAdd(a.tile_next, 1ull);
   const uint32_t lo = uint32_t(__shfl(uint32_t(c), 0, 64)), hi = uint32_t(__shfl(uint32_t(c >> 32), 0, 64));
-  return waves + ((uint64_t(hi) << 32) | lo);
+  return (uint64_t(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t next_tile(const ScanArgs& a, uint64_t t, uint64_t waves) {
+  // in-scan ordering: EVERY tile is claimed (see order_tile), none by index
+  if (a.out_line) return claim_tile(a);
+  if (!DGREP_DYNAMIC_TILES) return t + waves;
+  return waves + claim_tile(a);
+}
+__device__ __forceinline__ uint64_t first_tile(const ScanArgs& a, int tid, int NT) {
+  if (a.out_line) return claim_tile(a);
+  return uint64_t(blockIdx.x) * uint64_t(NT / 64) + uint64_t(tid >> 6);
+}
+
+// ---- in-scan ordering (single pass) -----------------------------------------
+// Without it, two passes after the scan place the tiles' staged lines
+// (tile_block_sum_kernel, order_lines_kernel: C3's 21.4 M records, 4 % of a
+// step). With ScanArgs::out_line set, each wave places a tile's lines itself:
+// at a tile's end it publishes the tile's aggregate (records, '\n'), and after
+// its NEXT tile (or at its end) it finds the tile's exclusive prefix by a
+// decoupled look-back over its predecessors' published aggregates / inclusive
+// prefixes, publishes its own inclusive prefix and copies the tile's staged
+// lines to their final slots -- while other waves still scan, so the copy
+// overlaps the scan's HBM stream. Deadlock-free: every tile is claimed from
+// the counter by a running wave (first_tile), a wave publishes a tile's
+// aggregate before it waits on anything, and the look-back waits only for
+// tiles claimed before the one it places.
+// Entries carry the launch's epoch (ScanArgs::epoch, never 0) in bits 48-63:
+// an entry of an earlier launch reads as not yet published, so nothing is
+// cleared between launches (the arrays are zeroed once, when allocated).
+//   agg[t]    = epoch | nl << 24 | count   (a tile's '\n' and records: < 2^23 each)
+//   incl_c[t] = epoch | records of tiles 0..t   (48 bits)
+//   incl_l[t] = epoch | '\n' of tiles 0..t      (48 bits)
+constexpr uint64_t kEpochShift = 48;
+constexpr uint64_t kVal48 = (1ull << kEpochShift) - 1ull;
+__device__ __forceinline__ uint64_t ld_dev(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_dev(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the exclusive prefix (records, '\n') of tile t, by the whole wave
+__device__ __forceinline__ void tile_prefix(const ScanArgs& a, uint64_t t, uint64_t& pc, uint64_t& pl) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t ep = uint64_t(a.epoch) << kEpochShift;
+  pc = 0;
+  pl = 0;
+  int64_t j = int64_t(t) - 1;  // the window is tiles j - 63 .. j, lane l at j - l
+  while (j >= 0) {
+    const int64_t jj = j - int64_t(lane);
+    const bool in = jj >= 0;
+    uint64_t ic = 0, il = 0, ag = 0;
+    bool vinc = false, vagg = false;
+    if (in) {
+      ic = ld_dev(a.incl_c + jj);
+      il = ld_dev(a.incl_l + jj);
+      vinc = (ic & ~kVal48) == ep && (il & ~kVal48) == ep;
+      if (!vinc) {
+        ag = ld_dev(a.agg + jj);
+        vagg = (ag & ~kVal48) == ep;
+      }
+    }
+    // the nearest predecessor with an inclusive prefix ends the walk; every
+    // tile after it needs its aggregate
+    const uint64_t minc = __ballot(in && vinc);
+    const uint32_t stop = minc ? uint32_t(__builtin_ctzll(minc)) : 64u;
+    const bool need = in && lane < stop;
+    if (__ballot(need && !vagg)) {
+      __builtin_amdgcn_s_sleep(4);  // a predecessor still scans: read the window again
+      continue;
+    }
+    uint64_t c = 0, l = 0;
+    if (need) {
+      c = ag & 0xffffffull;
+      l = (ag >> 24) & 0xffffffull;
+    } else if (in && lane == stop) {
+      c = ic & kVal48;
+      l = il & kVal48;
+    }
+    pc += wave_sum_u64_(c);
+    pl += wave_sum_u64_(l);
+    if (stop < 64u) break;
+    j -= 64;
+  }
+}
+
+// A tile scanned by this wave, waiting to be placed (wave-uniform).
+struct HeldTile {
+  uint64_t t;      // tile index (kNoTile: none)
+  uint64_t base;   // its first staged line
+  uint32_t count;  // its records
+  uint32_t nl;     // its '\n'
+};
+constexpr uint64_t kNoTile = ~0ull;
+
+__device__ __forceinline__ void publish_agg(const ScanArgs& a, uint64_t t, uint32_t count, uint32_t nl) {
+  if ((threadIdx.x & 63u) == 0)
+    st_dev(a.agg + t, (uint64_t(a.epoch) << kEpochShift) | (uint64_t(nl) << 24) | uint64_t(count));
+}
+
+// Place a held tile: its prefix, its inclusive prefix published, its staged
+// lines copied to their final SoA slots (line_no = 1 + '\n' before the line).
+__device__ __forceinline__ void order_tile(const ScanArgs& a, const HeldTile& h) {
+  uint64_t pc, pl;
+  tile_prefix(a, h.t, pc, pl);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (lane == 0) {
+    const uint64_t ep = uint64_t(a.epoch) << kEpochShift;
+    st_dev(a.incl_l + h.t, ep | ((pl + h.nl) & kVal48));
+    st_dev(a.incl_c + h.t, ep | ((pc + h.count) & kVal48));
+  }
+  // the staged lines were written by this wave a tile ago
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const uint64_t lb = pl + 1;
+  constexpr uint32_t U = 4;  // records per lane in flight
+  for (uint32_t k0 = 0; k0 < h.count; k0 += 64u * U) {
+    StagedLine L[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t k = k0 + u * 64u + lane;
+      if (k < h.count && h.base + k < a.capacity) L[u] = a.staging[h.base + k];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t k = k0 + u * 64u + lane;
+      const uint64_t dst = pc + k;
+      if (k < h.count && h.base + k < a.capacity && dst < a.out_cap) {
+        a.out_line[dst] = lb + staged_rel(L[u]);
+        a.out_start[dst] = L[u].start;
+        a.out_len[dst] = staged_len(L[u]);
+      }
+    }
+  }
 }
 
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
@@ -1359,7 +1555,8 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   // older waves): with a static stride the youngest waves set the kernel's
   // end. Same box, C2 pattern: 12 / 18 / 32 GiB splits ran 9 % below 16 GiB,
   // whose 2.67 rounds happened to give the young waves one tile less.
-  for (uint64_t t = uint64_t(blockIdx.x) * (NT / 64) + uint64_t(tid >> 6); t < a.ntiles; t = next_tile(a, t, waves)) {
+  HeldTile held{kNoTile, 0, 0, 0};  // in-scan ordering: the tile to place after this one
+  for (uint64_t t = first_tile(a, tid, NT); t < a.ntiles; t = next_tile(a, t, waves)) {
     uint64_t cs[S];
     LaneRun r[S];
     uint32_t nlc[S];
@@ -1431,10 +1628,10 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
       ti.nl = nl_tot;
       a.tiles[t] = ti;
     }
-    if (ev_tot == 0) continue;  // wave-uniform
+    if (a.out_line) publish_agg(a, t, ev_tot, nl_tot);
     base = (uint64_t(uint32_t(__shfl(uint32_t(base >> 32), 0, 64))) << 32) | uint32_t(__shfl(uint32_t(base), 0, 64));
 #pragma unroll
-    for (int k = 0; k < S; ++k) {
+    for (int k = 0; k < S && ev_tot != 0; ++k) {  // ev_tot: wave-uniform
       const uint32_t nev = r[k].nev;
       const uint32_t* sl = slots + k * E * 2;
       const bool spill = a.spill != nullptr;
@@ -1492,7 +1689,14 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         }
       }
     }
+    if (a.out_line) {
+      // place the tile scanned before this one (its predecessors are done by
+      // now, nearly always), then hold this one
+      if (held.t != kNoTile) order_tile(a, held);
+      held = HeldTile{t, base, ev_tot, nl_tot};
+    }
   }
+  if (held.t != kNoTile) order_tile(a, held);
 }
 
 // Lanes that owned more matching lines than their LDS slots are re-run here,

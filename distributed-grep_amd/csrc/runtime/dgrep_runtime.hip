@@ -52,6 +52,14 @@
 #ifndef DGREP_SHENG_MAPS
 #define DGREP_SHENG_MAPS 1
 #endif
+// A/B knob (off): the scan kernel places the lines itself (in-scan ordering,
+// scan_dfa.hip order_tile) instead of the two ordering passes after it,
+// whenever the speculative ordering applies (not the filter). Measured slower
+// on MI355X, same box (r05): C3 step 4.340 -> 4.357 ms, C2 3.380 -> 3.412 ms --
+// the placement added its time to the scan kernel's instead of hiding under it.
+#ifndef DGREP_SCAN_ORDER
+#define DGREP_SCAN_ORDER 0
+#endif
 
 namespace dgrep {
 // scan_dfa.hip
@@ -126,6 +134,11 @@ struct dgrep_ctx {
   uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0;
   StagedLine* d_staging = nullptr;
   uint64_t staging_cap = 0;
+  // in-scan ordering (ScanArgs::agg / incl_c / incl_l, 3 x order_cap entries,
+  // zeroed when allocated) and the epoch of the last launch (16 bits, never 0)
+  uint64_t* d_order = nullptr;
+  uint64_t order_cap = 0;
+  uint32_t epoch = 0;
   // device counters: [0] staging append counter, [1] overflow lanes, [2] parked
   // lines, [3] dropped candidates, [4] claimed tiles
   unsigned long long* d_counters = nullptr;
@@ -425,7 +438,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
-                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_seg_from, c->d_seg_state, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
+                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_seg_from, c->d_seg_state, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_order, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -947,6 +960,26 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   // Anything else shows in the counters, and the ordering is queued again once
   // the extra passes have run.
   const bool speculate = !filt && capacity != 0;
+  // in-scan ordering: the per-tile aggregate / prefix entries (zeroed once)
+  const bool in_scan = speculate && DGREP_SCAN_ORDER;
+  if (in_scan && c->order_cap < ntiles) {
+    if (c->d_order) HIPCHK(hipFree(c->d_order));
+    c->d_order = nullptr;
+    c->order_cap = 0;
+    const uint64_t cap = ntiles + ntiles / 8 + 64;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_order), 3 * cap * sizeof(uint64_t)));
+    HIPCHK(hipMemsetAsync(c->d_order, 0, 3 * cap * sizeof(uint64_t), c->stream));
+    c->order_cap = cap;
+  }
+  if (in_scan) {
+    a.out_line = d_line;
+    a.out_start = d_start;
+    a.out_len = d_len;
+    a.out_cap = capacity;
+    a.agg = c->d_order;
+    a.incl_c = c->d_order + c->order_cap;
+    a.incl_l = c->d_order + 2 * c->order_cap;
+  }
   // Each buffer a scan can outgrow (overflow list, pending list, the filter's
   // staging) is grown to what the scan counted and the scan re-run, so every
   // grow is followed by a scan that fits: at most three grows, four scans. (A
@@ -960,11 +993,15 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     a.overflow_cap = c->overflow_cap;
     a.pend = park ? c->d_pend : nullptr;
     a.pend_cap = park ? c->pend_cap : 0;
+    // a fresh epoch per launch (16 bits, never 0): the previous launch's
+    // ordering entries read as not yet published
+    c->epoch = c->epoch % 0xffffu + 1u;
+    a.epoch = c->epoch;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, kCounters * sizeof(unsigned long long), c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     HIPCHK(scan_dfa(c->step_kind, a, grid, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
-    if (speculate)
+    if (speculate && !in_scan)
       HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
                          d_line, d_start, d_len, c->stream));
     HIPCHK(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
@@ -1097,6 +1134,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   // the speculative ordering stands unless the overflow pass, the long-line
   // resolution or the verification changed the staged lines since
   const bool order = total != 0 && total <= capacity && (!speculate || over || verify);
+  S.order_in_scan = in_scan && !order ? 1u : 0u;
   if (order)
     HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
                        d_line, d_start, d_len, c->stream));

@@ -93,7 +93,8 @@ class _ScanStats(ctypes.Structure):
     _fields_ = [("stepper", ctypes.c_uint32), ("lane_chunk", ctypes.c_uint32), ("lane_slots", ctypes.c_uint32),
                 ("scan_attempts", ctypes.c_uint32), ("tiles", ctypes.c_uint64), ("overflow_lanes", ctypes.c_uint64),
                 ("matches", ctypes.c_uint64), ("scan_ms", ctypes.c_float), ("overflow_ms", ctypes.c_float),
-                ("verify_ms", ctypes.c_float), ("candidates", ctypes.c_uint64), ("pending", ctypes.c_uint64)]
+                ("verify_ms", ctypes.c_float), ("candidates", ctypes.c_uint64), ("pending", ctypes.c_uint64),
+                ("order_in_scan", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class _Gathered(ctypes.Structure):

@@ -278,6 +278,8 @@ typedef struct {
                               of the parked long lines */
   uint64_t candidates;     /* filter stepper: candidate lines dropped by that re-run */
   uint64_t pending;        /* Sheng: long lines parked by the scan and resolved from chunk maps */
+  uint32_t order_in_scan;  /* 1: the scan kernel placed the lines itself (no ordering pass ran after it) */
+  uint32_t reserved;
 } dgrep_scan_stats;
 int dgrep_last_scan_stats(dgrep_ctx* ctx, dgrep_scan_stats* out);
 

@@ -72,6 +72,30 @@ if durs:
             stats["%s_calls" % k] = len(v)
             post_mean += statistics.mean(v) * per_scan
             post_median += statistics.median(v) * per_scan
+# One bench step in the kernel trace: everything from one scan launch to the
+# next (ordering passes, counter read-back copies, memsets, host gaps), median
+# over the timed steps -- where the step time beyond the scan kernel goes.
+step_split = None
+if os.path.exists(tr_csv):
+    tr_rows = sorted(csv.DictReader(open(tr_csv)), key=lambda r: int(r["Start_Timestamp"]))
+    scans = [i for i, r in enumerate(tr_rows) if KERNEL in r["Kernel_Name"]]
+    steps = []
+    for i, j in zip(scans[-11:-1], scans[-10:]):
+        t0, t1 = int(tr_rows[i]["Start_Timestamp"]), int(tr_rows[j]["Start_Timestamp"])
+        parts = {}
+        busy = 0
+        for r in tr_rows[i:j]:
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "")
+            parts[name] = parts.get(name, 0) + d
+            busy += d
+        parts["idle (host sync, launch gaps)"] = (t1 - t0) - busy
+        parts["step"] = t1 - t0
+        steps.append(parts)
+    if steps:
+        keys = set().union(*steps)
+        step_split = {k: statistics.median([st.get(k, 0) for st in steps]) / 1e3 for k in sorted(keys)}
+        step_split["unit"] = "us, median over the last 10 scan-to-scan intervals"
 fetch = avg.get("FETCH_SIZE", 0.0) * 1024 * 2
 write = avg.get("WRITE_SIZE", 0.0) * 1024
 n = bench["config"]["split_bytes_per_gpu"]
@@ -92,6 +116,7 @@ summary = {
                             if "median_ns" in stats else None),
     "kernels_timed": [KERNEL] + [n for k, names in POST.items() if post[k] for n in names],
     "bench_hip_event_kernel_ms": bench["roofline"]["kernel_ms_avg"],
+    "step_split": step_split,
     "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 streaming-read half count), WRITE_SIZE KiB x1024",
 }
 json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)

@@ -18,4 +18,10 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "${PMC_BENCH[@]}" > /dev/null 2> "$OUT/pmc_write.err"
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc_sq" -o run -- python3 "${PMC_BENCH[@]}" > /dev/null 2> "$OUT/pmc_sq.err"
 timeout -s KILL 150 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_wait" -o run -- python3 "${PMC_BENCH[@]}" > /dev/null 2> "$OUT/pmc_wait.err"
+# DEEP=1: latency / instruction-mix / instruction-cache passes (Little's law:
+# SQ_INST_LEVEL_X / SQ_INSTS_X = mean cycles an X instruction is in flight)
+if [ "${DEEP:-0}" = 1 ]; then
+  timeout -s KILL 150 rocprofv3 --pmc SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_INST_LEVEL_LDS SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS --output-format csv -d "$OUT/pmc_lat" -o run -- python3 "${PMC_BENCH[@]}" > /dev/null 2> "$OUT/pmc_lat.err"
+  timeout -s KILL 150 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_IFETCH SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_icache" -o run -- python3 "${PMC_BENCH[@]}" > /dev/null 2> "$OUT/pmc_icache.err"
+fi
 echo "profile done: $OUT"
