@@ -37,7 +37,7 @@ FINAL_LINE_BYTES = 24   # the ABI's (u64 line_no, u64 start, u64 len) per match,
 def kernels_timed(stepper, in_scan):
     """The kernels dgrep_last_kernel_ms covers for this stepper (roofline.kernel)."""
     step = {"sheng": "StepSheng8", "pair": "StepPair", "table": "StepTable", "filter": "StepFilter",
-            "wide": "StepWide"}.get(stepper, str(stepper))
+            "wide": "StepWide", "word": "StepWord"}.get(stepper, str(stepper))
     ks = ["dgrep::scan_dfa8_kernel<dgrep::%s>%s" % (step, " (in-scan ordering)" if in_scan else "")]
     if stepper == "filter":
         ks.append("dgrep::verify_kernel (candidate lines on the whole DFA)")

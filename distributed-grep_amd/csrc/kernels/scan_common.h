@@ -110,6 +110,11 @@ struct ScanArgs {
   // kStepFilter only: the premultiplied CAND_END state (a '\n' ends a line that
   // left the LDS-resident part of the DFA: a candidate, verified afterwards)
   uint32_t cand_end;
+  // kStepWord only (byte offsets into the LDS image, see StepWord): the pair
+  // class table PC, the word class table WC (P x P), the word table TW and the
+  // single-byte table T1; bytes per TW row; pair classes; the lowest
+  // premultiplied event state (shadows, start_m) and recheck shadow
+  uint32_t wd_pb, wd_wc, wd_tw, wd_t1, wd_row, wd_thr_e, wd_thr_r;
   // one-chunk-per-lane steppers: per resident thread, spill_per_lane records of
   // HBM the lane moves its full LDS slots to (nullptr: no spilling)
   uint2* spill;
@@ -233,6 +238,7 @@ enum : int {
   kStepWide = 2,    // <= 65535 states: u16 [state][class] table, hot rows in LDS, all rows in HBM
   kStepPair = 3,    // 2 * states * classes^2 <= kPairMaxT2 bytes: two input bytes per table lookup
   kStepFilter = 4,  // > 256 states: the DFA's shallow part in LDS, lines that leave it verified afterwards
+  kStepWord = 5,    // one table lookup per 4-byte word: the DFA's word functions (few, for most regexes) in LDS
 };
 
 // LDS image of kStepFilter: byte classes [256] (u8), then u16 [state][class]
@@ -268,6 +274,11 @@ constexpr uint32_t kPairMaxT2 = 32768;
 #endif
 constexpr uint32_t kPairMaxImage = 40960;
 constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the byte tables)
+// StepWord's LDS image (u32 entries, see StepWord): UA, UB [256] at 0 / 1024,
+// PA [K][K] at kWordPA, PB [K][K], WC [P][P], TW [S'][W], T1 [S'][K]; at most
+// kWordMaxImage bytes.
+constexpr uint32_t kWordPA = 2048;
+constexpr uint32_t kWordMaxImage = 16384;
 
 // LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
 // runtime renumbers states hottest-first (start, start_m, then BFS order from

@@ -356,7 +356,10 @@ struct StepPair {
     s0 = s1;
     s2 = s3;
   }
-  // apply() in two parts: the word's first chain read, then the rest
+  // apply() in two parts: the word's first chain read, then the rest (f comes
+  // from a ds_read_u16; carried across the previous word's event branch it is
+  // re-masked by one v_and: neither __builtin_assume nor a v_mad_u32_u16 in
+  // asm removed it)
   __device__ __forceinline__ void rest(const Pre& p, uint32_t f, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                        uint32_t& s3) const {
     s1 = f;
@@ -376,6 +379,71 @@ struct StepPair {
     return uint32_t(s1 >= thr && s1 != M) | (uint32_t(s1 >= M) << 1) | (uint32_t(s3 >= thr && s3 != M) << 2) |
            (uint32_t(s3 >= M) << 3);
   }
+};
+
+// DFA with few WORD FUNCTIONS: ONE dependent table lookup per 4-byte word.
+// A word's effect on the DFA is a function S -> S; for the regexes of the
+// configs there are few distinct ones (C3's 20 states x 12 classes: 69 word
+// functions, 27 pair functions), so the runtime (build_word_image) numbers
+// them and the chain per word is s' = TW[s][w] -- one v_lshl_add + one
+// ds_read_u16 (pair stepper: two of each). The word class w depends only on
+// the input, in three table levels: byte classes C[b] (u8), pair classes
+// PC[c0][c1], word classes WC[p01][p23]; run_block_word issues those levels
+// words ahead of the chain, so they never wait on it.
+// Events: a word hides the states between its bytes, so a word whose single
+// '\n' ends a matching line before its last byte leads to an EVENT shadow (a
+// copy of the state its last bytes reach; a '\n' last in the word leaves
+// start_m itself), and a word with two or more '\n' leads to a RECHECK shadow
+// (its events are recomputed byte by byte from the state before it, rare).
+// Ids: the other states, the event shadows, start_m, the recheck shadows --
+// a word ending at >= thr_e holds an event or needs a recheck (>= thr_r).
+struct StepWord {
+  static constexpr int kKind = kStepWord;
+  // LDS image (u32 entries: a value crossing the event branch as a narrower
+  // load would be re-masked by a v_and on every use), at LDS address 0:
+  //   UA, UB [256]: 4 K class(b), 4 class(b)   -> pair index bytes UA[b0] + UB[b1]
+  //   PA, PB [K K] at kWordPA / pb:  4 P pc, 4 pc  -> word index bytes PA[..] + PB[..]
+  //   WC [P P] at wc: 4 w (the word's column bytes in TW)
+  //   TW [S'][W] at tw, rows of `row` bytes: the next state, premultiplied to its row's address
+  //   T1 [S'][K] at t1: single-byte steps, premultiplied
+  const uint8_t* lds;
+  const uint32_t* T1;
+  uint32_t K, pb, wc, thr_e, thr_r, row, tw;
+  __device__ __forceinline__ uint32_t ld(uint32_t a) const { return *reinterpret_cast<const uint32_t*>(lds + a); }
+  __device__ __forceinline__ uint32_t ua(uint32_t b) const { return ld(4u * b); }
+  __device__ __forceinline__ uint32_t ub(uint32_t b) const { return ld(1024u + 4u * b); }
+  __device__ __forceinline__ uint32_t pa(uint32_t ix) const { return ld(kWordPA + ix); }  // ix = UA + UB
+  __device__ __forceinline__ uint32_t pbv(uint32_t ix) const { return ld(pb + ix); }
+  __device__ __forceinline__ uint32_t wcol(uint32_t ix) const { return ld(wc + ix); }    // ix = PA + PB
+  // the stepper's one-word lookups run in run_block_word's pipeline; prep /
+  // apply serve the generic paths (cold starts, single words)
+  struct Pre {
+    uint32_t col;  // the word's column bytes in TW
+  };
+  __device__ __forceinline__ Pre prep(uint32_t x) const {
+    const uint32_t a = pa(ua(x & 0xffu) + ub((x >> 8) & 0xffu));
+    const uint32_t b = pbv(ua((x >> 16) & 0xffu) + ub(x >> 24));
+    return Pre{wcol(a + b)};
+  }
+  __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t col) const { return ld(s + col); }
+  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                        uint32_t& s3) const {
+    s3 = step(s, p.col);
+    s0 = s1 = s2 = s3;
+  }
+  // single-byte step (rare paths): state id = (premultiplied state - TW base) / row bytes
+  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
+    return T1[((s - tw) / row) * K + (ub(b) >> 2)];
+  }
+  // the exact states after each byte of word x from s (recheck / past-chunk paths)
+  __device__ __forceinline__ void bytes4(uint32_t s, uint32_t x, uint32_t& s0, uint32_t& s1, uint32_t& s2,
+                                         uint32_t& s3) const {
+    s0 = byte(s, x & 0xffu);
+    s1 = byte(s0, (x >> 8) & 0xffu);
+    s2 = byte(s1, (x >> 16) & 0xffu);
+    s3 = byte(s2, x >> 24);
+  }
+  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
 };
 
 // DFA of more than 256 states (large alternations, SURVEY config 4) as a
@@ -450,6 +518,11 @@ __device__ __forceinline__ StepPair make_step<StepPair>(const uint8_t* lds, cons
 }
 
 template <>
+__device__ __forceinline__ StepWord make_step<StepWord>(const uint8_t* lds, const ScanArgs& a) {
+  return StepWord{lds,      reinterpret_cast<const uint32_t*>(lds + a.wd_t1), a.nclasses, a.wd_pb, a.wd_wc,
+                  a.wd_thr_e, a.wd_thr_r, a.wd_row, a.wd_tw};
+}
+template <>
 __device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }
 template <>
 __device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds, const ScanArgs&) {
@@ -486,6 +559,14 @@ struct Tune<StepPair> {
   static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = DGREP_PAIR_STREAMS;
 };
 static_assert(Tune<StepPair>::B == 64 || Tune<StepPair>::B == 128, "block must be 64 or 128 bytes");
+// Word (C3): as the pair stepper, one chunk per lane, 128-B blocks (run_block_word)
+#ifndef DGREP_WORD_SLOTS
+#define DGREP_WORD_SLOTS 16
+#endif
+template <>
+struct Tune<StepWord> {
+  static constexpr int C = 4096, E = DGREP_WORD_SLOTS, B = 128, S = 1;
+};
 static_assert(Tune<StepPair>::C % Tune<StepPair>::B == 0 && Tune<StepPair>::C <= 32768, "bad pair chunk");
 static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
@@ -694,7 +775,7 @@ __device__ __forceinline__ uint32_t lnl_pos(uint32_t lnl) { return (lnl >> 3) - 
 // event path runs in ~27 % of words, and costs the Sheng stepper 1.8 % (C2,
 // profiles/r03/ablation/sentinel_c2.txt): a per-block init for a rare path.
 #ifndef DGREP_SENTINEL_KINDS
-#define DGREP_SENTINEL_KINDS ((1 << kStepPair) | (1 << kStepFilter) | (1 << kStepTable) | (1 << kStepWide))
+#define DGREP_SENTINEL_KINDS ((1 << kStepPair) | (1 << kStepFilter) | (1 << kStepTable) | (1 << kStepWide) | (1 << kStepWord))
 #endif
 template <class Step>
 constexpr bool sentinel() {
@@ -705,7 +786,8 @@ constexpr bool sentinel() {
 template <class Step, bool DIRECT>
 constexpr bool flat_emit() {
   // (not Filter: its 1024 threads x 8 B dummy would not fit beside its 124 KiB image)
-  return !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair) && Tune<Step>::S == 1;
+  return !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepWord) &&
+         Tune<Step>::S == 1;
 }
 
 // Everything a word step does after its four DFA steps s0..s3 (newline mask
@@ -865,6 +947,25 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
   word_nl<J>(m, b);
 }
 
+// StepWord: the events of word J (data x, states sp before it and se after
+// it). An event or recheck shows as se >= thr_e; a single '\n' inside the
+// chunk is the event (the shadow's meaning), anything else is recomputed byte
+// by byte from sp and takes word_emit's general loop.
+template <int J, int E, bool DIRECT>
+__device__ __forceinline__ void word_events_word(const StepWord& st, uint32_t M, uint32_t m, uint32_t x, uint32_t sp,
+                                                 uint32_t se, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
+  if (__builtin_expect(se >= st.thr_e, 0)) {
+    if (!b.past && (m & (m - 1u)) == 0u) {
+      word_emit<J>(st, M, m, se, se, se, se, b, r, emit);  // its fast path
+    } else {
+      uint32_t s0, s1, s2, s3;
+      st.bytes4(sp, x, s0, s1, s2, s3);
+      word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);  // its general loop
+    }
+  }
+  word_nl<J>(m, b);
+}
+
 template <bool SENT>
 __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const LaneRun& r) {
   b.pos = pos;
@@ -982,6 +1083,89 @@ __device__ __forceinline__ void run_block_pipe(const Step& st, uint32_t M, const
   DG_WP(24) DG_WP(25) DG_WP(26) DG_WP(27) DG_WP(28) DG_WP(29) DG_WP(30) DG_WP(31)
 #undef DG_WP
   blk_finish(b, s, r);
+}
+
+// StepWord's lookahead, carried from block to block (see run_block_word).
+// Entering word J: f = word J's chain read (in flight); c1 = word J+1's column
+// bytes; a2/b2 = word J+2's pair entries (PA, PB); x3[4] = word J+3's byte
+// entries (UA, UB, UA, UB).
+struct WordPipe {
+  uint32_t f, c1, a2, b2;
+  uint32_t x3[4];
+  bool warm;
+};
+__device__ __forceinline__ void word_bytes_cls(const StepWord& st, uint32_t x, uint32_t (&c)[4]) {
+  c[0] = st.ua(x & 0xffu);
+  c[1] = st.ub((x >> 8) & 0xffu);
+  c[2] = st.ua((x >> 16) & 0xffu);
+  c[3] = st.ub(x >> 24);
+}
+
+// One block of StepWord: per word ONE dependent LDS read on the chain. Word
+// J's step, LDS reads completing in issue order:
+//   wait f (word J's state); issue word J+1's chain read (state + c1) FIRST;
+//   then the table levels, each from the level the previous step issued
+//   (complete a few LDS cycles after that step's chain read): word J+2's
+//   column (WC), word J+3's pair entries (PA, PB), word J+4's byte entries;
+//   then word J's events and newline bookkeeping, under the chain read.
+// Words past the block come from the next block's registers (nx).
+template <int BK, int E, bool DIRECT>
+__device__ __forceinline__ void run_block_word(const StepWord& st, uint32_t M, const uint4 (&v)[BK / 16],
+                                               const uint4 (&nx)[BK / 16], uint64_t pos, uint64_t C, LaneRun& r,
+                                               const Emitter<E, DIRECT>& emit, WordPipe& q) {
+  static_assert(BK == 128, "the word stepper's lookahead is laid out for 128-byte blocks");
+  Blk b;
+  blk_init<true>(b, pos, C, r);
+  constexpr int NW = BK / 4;
+  uint32_t w[NW + 4];
+#pragma unroll
+  for (int i = 0; i < BK / 16; ++i) {
+    w[4 * i + 0] = v[i].x;
+    w[4 * i + 1] = v[i].y;
+    w[4 * i + 2] = v[i].z;
+    w[4 * i + 3] = v[i].w;
+  }
+  w[NW + 0] = nx[0].x;
+  w[NW + 1] = nx[0].y;
+  w[NW + 2] = nx[0].z;
+  w[NW + 3] = nx[0].w;
+  if (!q.warm) {
+    // cold start (a lane's first block): the lookahead of words 0-3
+    const uint32_t c0 = st.prep(w[0]).col;
+    q.c1 = st.prep(w[1]).col;
+    uint32_t x2[4];
+    word_bytes_cls(st, w[2], x2);
+    q.a2 = st.pa(x2[0] + x2[1]);
+    q.b2 = st.pbv(x2[2] + x2[3]);
+    word_bytes_cls(st, w[3], q.x3);
+    q.f = st.step(r.s, c0);
+    q.warm = true;
+  }
+  uint32_t sp = r.s;
+#define DG_WW(J)                                                                          \
+  {                                                                                       \
+    const uint32_t sJ = q.f;                                                              \
+    q.f = st.step(sJ, q.c1); /* word J+1's chain read */                                 \
+    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
+    const uint32_t c2 = st.wcol(q.a2 + q.b2);                                             \
+    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
+    const uint32_t a3 = st.pa(q.x3[0] + q.x3[1]), b3 = st.pbv(q.x3[2] + q.x3[3]);         \
+    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
+    word_bytes_cls(st, w[(J) + 4], q.x3);                                                 \
+    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
+    const uint32_t m = nl_mask(w[J]);                                                     \
+    word_events_word<J>(st, M, m, w[J], sp, sJ, b, r, emit);                              \
+    sp = sJ;                                                                              \
+    q.c1 = c2;                                                                            \
+    q.a2 = a3;                                                                            \
+    q.b2 = b3;                                                                            \
+  }
+  DG_WW(0) DG_WW(1) DG_WW(2) DG_WW(3) DG_WW(4) DG_WW(5) DG_WW(6) DG_WW(7)
+  DG_WW(8) DG_WW(9) DG_WW(10) DG_WW(11) DG_WW(12) DG_WW(13) DG_WW(14) DG_WW(15)
+  DG_WW(16) DG_WW(17) DG_WW(18) DG_WW(19) DG_WW(20) DG_WW(21) DG_WW(22) DG_WW(23)
+  DG_WW(24) DG_WW(25) DG_WW(26) DG_WW(27) DG_WW(28) DG_WW(29) DG_WW(30) DG_WW(31)
+#undef DG_WW
+  blk_finish(b, sp, r);
 }
 
 template <int BK, bool MAP, class Step, int E, bool DIRECT>
@@ -1116,7 +1300,7 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
 template <class Step, bool DIRECT>
 constexpr bool track_long() {
   return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepTable ||
-          (Step::kKind == kStepFilter && DGREP_FILTER_PARK)) &&
+          Step::kKind == kStepWord || (Step::kKind == kStepFilter && DGREP_FILTER_PARK)) &&
          !DIRECT;
 }
 // the parked state as an index of ScanArgs::pend_states (stepper encoding ->
@@ -1125,6 +1309,7 @@ template <class Step>
 __device__ __forceinline__ uint32_t park_index(const ScanArgs& a, uint32_t s) {
   if constexpr (Step::kKind == kStepSheng8) return s & 0xffu;
   else if constexpr (Step::kKind == kStepPair) return (s - Step::kT2) / a.pair_div;
+  else if constexpr (Step::kKind == kStepWord) return (s - a.wd_tw) / a.wd_row;
   else if constexpr (Step::kKind == kStepFilter) return 0;  // re-run from the line start
   else return s;
 }
@@ -1214,8 +1399,12 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   const bool maps = kMap && emit.cmap != nullptr;
   if (maps && pos0 == 0) *emit.mapsl = make_uint2(0x03020100u, 0x07060504u);  // identity
   if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
-#define DG_STEP(V)                                                                         \
-  if (kMap && __ballot(maps && r.nl == 0u && pos >= kLazyMapBytes && pos < uint64_t(C)) != 0) \
+  WordPipe wp;  // StepWord: the lookahead carried from block to block
+  wp.warm = false;
+#define DG_STEP(V, NX)                                                                     \
+  if constexpr (Step::kKind == kStepWord)                                                  \
+    run_block_word<BK>(st, M, V, NX, pos, uint64_t(C), r, emit, wp);                       \
+  else if (kMap && __ballot(maps && r.nl == 0u && pos >= kLazyMapBytes && pos < uint64_t(C)) != 0) \
     run_block<BK, kMap>(st, M, V, pos, uint64_t(C), r, emit);                              \
   else                                                                                     \
     run_block<BK, false>(st, M, V, pos, uint64_t(C), r, emit);
@@ -1266,11 +1455,11 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   for (;;) {
     DG_CHECK
     load_block<BK>(B, p + (pos + 2 * BK <= avail ? pos + BK : pos));  // prefetch (or a harmless re-read)
-    DG_STEP(A)
+    DG_STEP(A, B)
     pos += BK;
     DG_CHECK
     load_block<BK>(A, p + (pos + 2 * BK <= avail ? pos + BK : pos));
-    DG_STEP(B)
+    DG_STEP(B, A)
     pos += BK;
   }
 #undef DG_STEP
@@ -1327,7 +1516,8 @@ __device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uin
 // (run_lane2) is compiled for Tune::C.
 template <class Step, int TBL>
 constexpr bool adaptive_chunk() {
-  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepFilter) &&
+  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepFilter ||
+          Step::kKind == kStepWord) &&
          streams_of<Step, TBL>() == 1;
 }
 template <class Step, int TBL>
@@ -1372,7 +1562,7 @@ template <class Step>
 constexpr int waves_per_simd() {
   return Step::kKind == kStepSheng8  ? DGREP_SHENG_WAVES
          : Step::kKind == kStepTable ? DGREP_TABLE_WAVES
-         : Step::kKind == kStepPair  ? DGREP_PAIR_WAVES
+         : Step::kKind == kStepPair || Step::kKind == kStepWord ? DGREP_PAIR_WAVES
                                      : Step::kKind == kStepFilter ? kFilterThreads / 256
                                                                   : kWideThreads / 256;  // one workgroup per CU
 }
@@ -2557,6 +2747,11 @@ constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
 // 32 KiB beat 16 KiB (profiles/r04/ablation/chunk_dyn.txt).
 // The filter stops at 32 KiB (64 KiB chunks were measured on the Sheng
 // stepper's access pattern only).
+// The word stepper starts from the pair stepper's 8 KiB (same slots, same
+// event density).
+#ifndef DGREP_WORD_MAX_CHUNK
+#define DGREP_WORD_MAX_CHUNK 8192
+#endif
 #ifndef DGREP_FILTER_MAX_CHUNK
 #define DGREP_FILTER_MAX_CHUNK 32768
 #endif
@@ -2599,6 +2794,7 @@ struct TileOp {
       c = force ? uint64_t(force)
                 : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap,
                                        S::kKind == kStepPair     ? DGREP_PAIR_MAX_CHUNK
+                                       : S::kKind == kStepWord   ? DGREP_WORD_MAX_CHUNK
                                        : S::kKind == kStepFilter ? DGREP_FILTER_MAX_CHUNK
                                                                  : kShengMaxChunk,
                                        // the filter keeps 32 KiB at 2 tiles per wave (C4: 16 KiB -1.5 %)
@@ -2635,7 +2831,11 @@ hipError_t part_sheng(int, uint32_t, const Op& op) {
   return op.template run<StepSheng8, 2048>();
 }
 template <class Op>
-hipError_t part_pair(int, uint32_t table_bytes, const Op& op) {
+hipError_t part_pair(int kind, uint32_t table_bytes, const Op& op) {
+  if (kind == kStepWord) {
+    if (table_bytes <= 8192) return op.template run<StepWord, 8192>();
+    return op.template run<StepWord, int(kWordMaxImage)>();
+  }
   if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
   if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB)
   if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
@@ -2686,7 +2886,7 @@ DG_OPS(extern template, part_big)
 template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, const Op& op) {
   if (kind == kStepSheng8) return part_sheng(kind, table_bytes, op);
-  if (kind == kStepPair) return part_pair(kind, table_bytes, op);
+  if (kind == kStepPair || kind == kStepWord) return part_pair(kind, table_bytes, op);
   if (kind == kStepWide || kind == kStepFilter) return part_big(kind, table_bytes, op);
   return part_table(kind, table_bytes, op);
 }
@@ -2702,7 +2902,7 @@ uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t re
   (void)dispatch(kind, table_bytes,
                  TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots, spill_per_lane});
   *threads = *waves_per_block * 64;
-  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepFilter;
+  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepFilter || kind == kStepWord;
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {

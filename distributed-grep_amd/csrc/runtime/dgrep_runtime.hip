@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -31,6 +32,15 @@
 #endif
 // DFAs above the Sheng limit whose two-byte table fits in LDS use the pair
 // stepper (0: they use the u8 table / wide steppers as before)
+// the word stepper (one lookup per 4 bytes) as the default for > 8-state DFAs
+// whose word tables fit (A/B knob). Off: measured slower than the pipelined
+// pair stepper on C3, same box (r05): kernel 0.507-0.512 vs 0.543 of HBM peak
+// -- its eight LDS reads per word (four byte classes, two pair classes, the
+// word class, the chain) cost more than the one chain read it saves. Forced
+// with dgrep_set_stepper(ctx, 5, 0).
+#ifndef DGREP_WORD_ENABLE
+#define DGREP_WORD_ENABLE 0
+#endif
 #ifndef DGREP_PAIR_ENABLE
 #define DGREP_PAIR_ENABLE 1
 #endif
@@ -89,6 +99,11 @@ using namespace dgrep;
 constexpr size_t kCounters = 8;
 
 // StepPair image offsets and thresholds (see StepPair in scan_dfa.hip)
+// the word stepper's LDS offsets and thresholds (build_word_image)
+struct WordArgs {
+  uint32_t pb, wc, tw, t1, row, thr_e, thr_r;
+  uint32_t W, P;
+};
 struct PairArgs {
   uint32_t t1 = 0, thr = 0, div = 0;
 };
@@ -115,6 +130,7 @@ struct dgrep_ctx {
   uint32_t lane_chunk = 0;  // dgrep_set_lane_chunk (0 = adaptive)
   int step_kind = kStepTable;
   PairArgs pair_args;
+  WordArgs word_args{};
   // kStepFilter: CAND_END (premultiplied), and the whole DFA for verify_kernel
   uint32_t cand_end = UINT32_MAX;
   void* d_full = nullptr;      // [nstates][nclasses], the blob's ids: u16, or u32 above 65535 states
@@ -323,6 +339,126 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   return true;
 }
 
+// The word stepper's LDS image (StepWord, scan_dfa.hip): the DFA's effect of
+// every 4-byte word of byte classes (K^4 of them) as a function on the states,
+// extended by the event rule -- a word whose single '\n' enters start_m before
+// its last byte leads to an EVENT shadow of the state it ends in, a word with
+// two or more '\n' to a RECHECK shadow -- numbered into W word classes; pair
+// classes (pairs of byte classes equivalent in either half of every word) make
+// the word class a two-level lookup WC[PA(b0, b1) + PB(b2, b3)]. Ids: the
+// states other than start_m, the event shadows, start_m, the recheck shadows;
+// u32 entries, states premultiplied to their TW row's address. Returns false
+// if the DFA does not fit (kWordMaxImage bytes, K <= 32, S <= 255).
+bool build_word_image(const dgrep_blob_header& h, const uint32_t* trans, std::vector<uint8_t>* img, uint32_t* start,
+                      uint32_t* start_m, WordArgs* wa, std::vector<uint32_t>* orig_out) {
+  const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
+  const uint32_t cn = h.byte_class[uint8_t('\n')];
+  if (K > 32 || S > 255 || S < 2) return false;
+  const uint64_t K2 = uint64_t(K) * K, K4 = K2 * K2;
+  if (K4 * S > (uint64_t(1) << 24)) return false;
+  auto T = [&](uint32_t s, uint32_t c) { return trans[size_t(s) * K + c]; };
+  // per quad of classes and start state: x (plain), S + x (event shadow of x),
+  // 2 S + x (recheck shadow of x)
+  std::vector<uint32_t> F(size_t(K4) * S);
+  for (uint64_t q = 0; q < K4; ++q) {
+    const uint32_t c[4] = {uint32_t(q / (K2 * K)), uint32_t(q / K2 % K), uint32_t(q / K % K), uint32_t(q % K)};
+    const int nl = int(c[0] == cn) + int(c[1] == cn) + int(c[2] == cn) + int(c[3] == cn);
+    for (uint32_t s = 0; s < S; ++s) {
+      uint32_t x = s;
+      bool ev = false;
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t y = T(x, c[k]);
+        if (c[k] == cn && y == M && k < 3) ev = true;
+        x = y;
+      }
+      F[size_t(q) * S + s] = nl >= 2 ? 2 * S + x : (nl == 1 && ev ? S + x : x);
+    }
+  }
+  // word classes
+  std::map<std::vector<uint32_t>, uint32_t> wid;
+  std::vector<uint32_t> wq(K4), wrep;
+  for (uint64_t q = 0; q < K4; ++q) {
+    std::vector<uint32_t> f(F.begin() + size_t(q) * S, F.begin() + size_t(q + 1) * S);
+    auto it = wid.find(f);
+    if (it == wid.end()) {
+      it = wid.emplace(std::move(f), uint32_t(wrep.size())).first;
+      wrep.push_back(uint32_t(q));
+    }
+    wq[q] = it->second;
+  }
+  const uint32_t W = uint32_t(wrep.size());
+  // pair classes: pairs with the same word class in the first and in the
+  // second half of every word
+  std::map<std::vector<uint32_t>, uint32_t> pid;
+  std::vector<uint32_t> pc(K2);
+  for (uint64_t x = 0; x < K2; ++x) {
+    std::vector<uint32_t> sig(2 * K2);
+    for (uint64_t z = 0; z < K2; ++z) {
+      sig[z] = wq[x * K2 + z];
+      sig[K2 + z] = wq[z * K2 + x];
+    }
+    auto it = pid.emplace(std::move(sig), uint32_t(pid.size())).first;
+    pc[x] = it->second;
+  }
+  const uint32_t P = uint32_t(pid.size());
+  // ids
+  std::vector<uint8_t> is_e(S, 0), is_r(S, 0);
+  for (uint32_t v : F) {
+    if (v >= 2 * S) is_r[v - 2 * S] = 1;
+    else if (v >= S) is_e[v - S] = 1;
+  }
+  std::vector<uint32_t> id(S), eid(S, UINT32_MAX), rid(S, UINT32_MAX), orig;
+  for (uint32_t x = 0; x < S; ++x)
+    if (x != M) { id[x] = uint32_t(orig.size()); orig.push_back(x); }
+  const uint32_t first_e = uint32_t(orig.size());
+  for (uint32_t x = 0; x < S; ++x)
+    if (is_e[x]) { eid[x] = uint32_t(orig.size()); orig.push_back(x); }
+  id[M] = uint32_t(orig.size());
+  orig.push_back(M);
+  const uint32_t first_r = uint32_t(orig.size());
+  for (uint32_t x = 0; x < S; ++x)
+    if (is_r[x]) { rid[x] = uint32_t(orig.size()); orig.push_back(x); }
+  const uint32_t Sp = uint32_t(orig.size());
+  // layout (bytes)
+  const uint32_t pa = kWordPA, pb = pa + 4 * uint32_t(K2), wc = pb + 4 * uint32_t(K2);
+  const uint32_t tw = (wc + 4 * P * P + 15) & ~15u;
+  const uint32_t row = 4 * (W | 1u);  // an odd number of dwords: same column, different banks
+  const uint64_t t1 = (uint64_t(tw) + uint64_t(row) * Sp + 15) & ~uint64_t(15);
+  const uint64_t end = (t1 + 4ull * Sp * K + 15) & ~uint64_t(15);
+  if (end > kWordMaxImage) return false;
+  img->assign(end, 0);
+  auto put = [&](uint64_t off, uint32_t v) { memcpy(img->data() + off, &v, 4); };
+  auto premul = [&](uint32_t i) { return tw + i * row; };
+  auto code_id = [&](uint32_t v) { return v >= 2 * S ? rid[v - 2 * S] : v >= S ? eid[v - S] : id[v]; };
+  for (int b = 0; b < 256; ++b) {
+    put(4 * b, 4 * K * h.byte_class[b]);
+    put(1024 + 4 * b, 4 * h.byte_class[b]);
+  }
+  for (uint64_t x = 0; x < K2; ++x) {
+    put(pa + 4 * x, 4 * P * pc[x]);
+    put(pb + 4 * x, 4 * pc[x]);
+  }
+  for (uint64_t x = 0; x < K2; ++x)
+    for (uint64_t z = 0; z < K2; ++z) put(wc + 4 * (uint64_t(pc[x]) * P + pc[z]), 4 * wq[x * K2 + z]);
+  for (uint32_t i = 0; i < Sp; ++i) {
+    for (uint32_t w = 0; w < W; ++w) put(tw + uint64_t(i) * row + 4 * w, premul(code_id(F[size_t(wrep[w]) * S + orig[i]])));
+    for (uint32_t c = 0; c < K; ++c) put(t1 + 4 * (uint64_t(i) * K + c), premul(id[T(orig[i], c)]));
+  }
+  *start = premul(id[h.start]);
+  *start_m = premul(id[M]);
+  wa->pb = pb;
+  wa->wc = wc;
+  wa->tw = tw;
+  wa->t1 = uint32_t(t1);
+  wa->row = row;
+  wa->thr_e = premul(first_e);
+  wa->thr_r = premul(first_r);
+  wa->W = W;
+  wa->P = P;
+  *orig_out = orig;  // word state index -> blob state (a shadow -> the state it copies)
+  return true;
+}
+
 // The filter stepper's LDS image (StepFilter, scan_dfa.hip): byte classes (kFilterClassBytes),
 // then u16 rows of the DFA's first
 // R - 2 states in breadth-first order from start (start_m at depth 0), as many
@@ -484,7 +620,7 @@ extern "C" int dgrep_set_lane_chunk(dgrep_ctx* c, uint32_t chunk_bytes) {
 }
 
 extern "C" int dgrep_set_stepper(dgrep_ctx* c, int force, uint32_t wide_hot_rows) {
-  if (!c || force < 0 || force > 4) return DGREP_E_INVALID;
+  if (!c || force < 0 || force > 5) return DGREP_E_INVALID;
   c->force_stepper = force;
   c->wide_hot_rows_cap = wide_hot_rows ? wide_hot_rows : UINT32_MAX;
   return DGREP_OK;
@@ -521,7 +657,15 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   std::vector<uint8_t> pair_img;
   uint32_t pair_start = 0, pair_m = 0;
   std::vector<uint32_t> st2id;  // stepper state index -> blob state (long lines, see resolve_long_lines)
-  const bool want_pair = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3);
+  // the word stepper first (one lookup per 4 bytes), then the pair stepper
+  const bool want_word = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_WORD_ENABLE) || force == 5);
+  const bool word_ok = want_word && build_word_image(h, trans, &pair_img, &pair_start, &pair_m, &c->word_args, &st2id);
+  if (force == 5 && !word_ok) {
+    c->err = "dgrep_load_dfa: the word stepper's tables do not fit this DFA";
+    return DGREP_E_UNSUPPORTED;
+  }
+  const bool want_pair =
+      !partial && !word_ok && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3);
   const bool pair_ok = want_pair && build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args, &st2id);
   if (force == 3 && !pair_ok) {
     c->err = "dgrep_load_dfa: the pair stepper's two-byte table does not fit this DFA";
@@ -529,15 +673,15 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   }
   std::vector<uint8_t> filter_img;
   uint32_t f_start = 0, f_m = 0, f_cend = UINT32_MAX;
-  const bool filter_ok = !pair_ok && ((force == 0 && (h.nstates > 256 || partial)) || force == 4) &&
+  const bool filter_ok = !pair_ok && !word_ok && ((force == 0 && (h.nstates > 256 || partial)) || force == 4) &&
                          build_filter_image(h, trans, c->wide_hot_rows_cap, &filter_img, &f_start, &f_m, &f_cend,
                                             partial ? h.nstates - 1 : UINT32_MAX);
   if ((force == 4 || partial) && !filter_ok) {
     c->err = "dgrep_load_dfa: the filter stepper cannot hold this DFA's first states";
     return DGREP_E_UNSUPPORTED;
   }
-  if (pair_ok) {
-    c->step_kind = kStepPair;
+  if (word_ok || pair_ok) {
+    c->step_kind = word_ok ? kStepWord : kStepPair;
     c->nclasses = h.nclasses;
     t.swap(pair_img);
     start = pair_start;
@@ -555,7 +699,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_nfa = nullptr;
   if (c->d_full) HIPCHK(hipFree(c->d_full));
   c->d_full = nullptr;
-  if (pair_ok) {
+  if (pair_ok || word_ok) {
     // image built above
   } else if (filter_ok && partial) {
     const uint32_t* prog = trans + size_t(h.nstates) * h.nclasses;
@@ -695,7 +839,9 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_long_tbl = nullptr;
   c->d_st2id = nullptr;
   c->long_states = 0;
-  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepTable) && h.nstates <= 256 &&
+  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepTable ||
+       c->step_kind == kStepWord) &&
+      h.nstates <= 256 &&
       !st2id.empty()) {
     std::vector<uint8_t> lt(size_t(h.nstates) * 256);
     for (uint32_t s = 0; s < h.nstates; ++s)
@@ -938,6 +1084,13 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.wide = c->d_wide;
   a.nclasses = c->nclasses;
   a.hot_entries = c->hot_entries;
+  a.wd_pb = c->word_args.pb;
+  a.wd_wc = c->word_args.wc;
+  a.wd_tw = c->word_args.tw;
+  a.wd_t1 = c->word_args.t1;
+  a.wd_row = c->word_args.row;
+  a.wd_thr_e = c->word_args.thr_e;
+  a.wd_thr_r = c->word_args.thr_r;
   a.pair_t1 = c->pair_args.t1;
   a.pair_thr = c->pair_args.thr;
   a.pair_div = c->pair_args.div;

@@ -60,7 +60,7 @@ EXPORTS = (
 )
 COMM_ID_BYTES = 128
 
-STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair", 4: "filter"}
+STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair", 4: "filter", 5: "word"}
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
 
@@ -301,7 +301,7 @@ class Context:
         (dgrep_set_lane_chunk; 0 = adaptive)."""
         self._check(self._L.dgrep_set_lane_chunk(self._h, chunk_bytes))
 
-    _FORCE = {"auto": 0, "wide": 1, "table": 2, "pair": 3, "filter": 4}
+    _FORCE = {"auto": 0, "wide": 1, "table": 2, "pair": 3, "filter": 4, "word": 5}
 
     def set_stepper(self, force=False, wide_hot_rows: int = 0):
         """Testing/tuning: the stepper the next load() uses (dgrep_set_stepper):

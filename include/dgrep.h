@@ -119,7 +119,9 @@ int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
  * force: 0 = that default, 1 = wide (u16, LDS-hot + HBM) for any DFA, 2 = the
  * u8 table (<= 256 states), 3 = pair (dgrep_load_dfa fails with
  * DGREP_E_UNSUPPORTED if it does not fit), 4 = filter (the default above 256
- * states). wide_hot_rows != 0 caps the LDS-resident rows of the wide stepper
+ * states), 5 = word (one lookup per 4-byte word; the default for > 8-state DFAs
+ * whose word tables fit; DGREP_E_UNSUPPORTED if they do not). wide_hot_rows != 0
+ * caps the LDS-resident rows of the wide stepper
  * and of the filter (whose cut then sends nearly every line to verification). */
 int dgrep_set_stepper(dgrep_ctx* ctx, int force, uint32_t wide_hot_rows);
 /* Tests / tuning: lane chunk of the Sheng (<= 8-state) and pair steppers for
@@ -265,7 +267,8 @@ int dgrep_last_kernel_ms(dgrep_ctx* ctx, float* ms);
 /* What the last dgrep_scan* call did (tests, tuning, bench reports). */
 typedef struct {
   uint32_t stepper;        /* 0 u8 table, 1 Sheng (<= 8 states), 2 wide u16 table, 3 pair (two bytes per lookup),
-                              4 filter (shallow DFA states in LDS + candidate verification) */
+                              4 filter (shallow DFA states in LDS + candidate verification), 5 word (four bytes
+                              per lookup) */
   uint32_t lane_chunk;     /* bytes per lane chunk */
   uint32_t lane_slots;     /* LDS slots per lane chunk for matching lines */
   uint32_t scan_attempts;  /* scan launches (2 if the overflow list had to grow) */

@@ -140,7 +140,7 @@ def test_lane_chunk_validation(gpu_ctx):
     gpu_ctx.set_lane_chunk(0)
 
 
-@pytest.mark.parametrize("stepper", ["auto", "pair", "filter"])
+@pytest.mark.parametrize("stepper", ["auto", "pair", "filter", "word"])
 @pytest.mark.parametrize("chunk", [32768, 65536])
 def test_lines_starting_at_chunk_end(gpu_ctx, stepper, chunk):
     """A lane's last owned line can start exactly AT its chunk end (the chunk's
@@ -582,22 +582,38 @@ PAIR_PATTERNS = [b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"(WARN|ERROR) [a-
                  b"[^a-z ]{3}", b"^$|error", b"x*$|WARN"]
 
 
-@pytest.fixture
-def pair_ctx(gpu_ctx):
-    # the pair stepper also for DFAs the default gives to Sheng (<= 8 states)
-    gpu_ctx.set_stepper("pair")
+@pytest.fixture(params=["pair", "word"])
+def pair_ctx(gpu_ctx, request):
+    # the pair stepper (two bytes per lookup) and the word stepper (four), also
+    # for DFAs the default gives to Sheng (<= 8 states)
+    gpu_ctx.set_stepper(request.param)
+    gpu_ctx.test_mode = request.param
     yield gpu_ctx
     gpu_ctx.set_stepper("auto")
+
+
+def _load_mode(ctx, pattern):
+    """ctx.load, skipping a pattern whose tables the forced stepper cannot hold
+    (the word stepper's word tables, for a few patterns: the default then picks
+    the pair stepper)."""
+    import dgrep
+
+    try:
+        return ctx.load(pattern)
+    except dgrep.UnsupportedPattern:
+        if getattr(ctx, "test_mode", "") == "word":
+            pytest.skip("word tables do not fit: %r" % pattern)
+        raise
 
 
 @pytest.mark.parametrize("pattern", PAIR_PATTERNS + [b"error", b"", b"^$", b"(?i)k", b"\\x{FFFD}"])
 def test_pair_stepper_edges_and_random(pair_ctx, pattern):
     gpu_ctx = pair_ctx
-    cp = gpu_ctx.load(pattern)
+    cp = _load_mode(gpu_ctx, pattern)
     for data in [b"", b"\n", b"\n\n", b"\n\n\n", b"x", b"x\n", b"\nx", b"error\n\nerror", b"key\nk\n",
                  b"\xff\xfe\n\xe2\x82\xac\n\xe2\x82\n", b"a" * 5000 + b"WARN ab" + b"b" * 5000 + b"\nerror"]:
         _check(gpu_ctx, cp, data)
-        assert gpu_ctx.scan_stats()["stepper"] == "pair", pattern
+        assert gpu_ctx.scan_stats()["stepper"] == gpu_ctx.test_mode, pattern
     rnd = random.Random(hash(pattern) & 0xffff)
     alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\n\n", b"\r",
              b"\xe2\x82\xac", b"\xff", b"WARN ab", b"ERROR x", b"error", b"2024-01-02", b"key "]
@@ -625,10 +641,10 @@ def test_pair_stepper_chunk_and_tile_edges(pair_ctx, chunk):
                 data[2 * chunk:2 * chunk + 8] = b" WARN ab"
             data = bytes(data)
             for pattern in (b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"^$|ok$", b"(WARN|ERROR) [a-z_]+"):
-                cp = gpu_ctx.load(pattern)
+                cp = _load_mode(gpu_ctx, pattern)
                 _check(gpu_ctx, cp, data)
                 st = gpu_ctx.scan_stats()
-                assert st["stepper"] == "pair" and st["lane_chunk"] == chunk, st
+                assert st["stepper"] == gpu_ctx.test_mode and st["lane_chunk"] == chunk, st
     finally:
         gpu_ctx.set_lane_chunk(0)
 
@@ -638,12 +654,12 @@ def test_pair_stepper_dense_overflow(pair_ctx):
     for maxlen in (2, 5, 40, 700):
         data = _dense_lines(maxlen + 1, 40000 if maxlen < 100 else 6000, maxlen)
         for pattern in (b"(WARN|ERROR) [a-z_]+", b"^$|error", b"b x*$"):
-            cp = gpu_ctx.load(pattern)
+            cp = _load_mode(gpu_ctx, pattern)
             _check(gpu_ctx, cp, data)
-            assert gpu_ctx.scan_stats()["stepper"] == "pair"
+            assert gpu_ctx.scan_stats()["stepper"] == gpu_ctx.test_mode
     data2 = b"\n" * 100001
     for pattern in (b"^$|error", b"a|^$"):
-        _check(gpu_ctx, pattern, data2)
+        _check(gpu_ctx, _load_mode(gpu_ctx, pattern), data2)
 
 
 @pytest.mark.parametrize("chunk", [4096, 32768])
@@ -667,15 +683,15 @@ def test_pair_deferred_events_line_shapes(pair_ctx, chunk):
     try:
         gpu_ctx.set_lane_chunk(chunk)
         for pattern in (b"(WARN|ERROR) [a-z_]+", b"^$|b$", b"WARN ab"):
-            cp = gpu_ctx.load(pattern)
+            cp = _load_mode(gpu_ctx, pattern)
             _check(gpu_ctx, cp, data)
             _check(gpu_ctx, cp, data[: len(data) // 2 + 13])
-            assert gpu_ctx.scan_stats()["stepper"] == "pair"
+            assert gpu_ctx.scan_stats()["stepper"] == gpu_ctx.test_mode
     finally:
         gpu_ctx.set_lane_chunk(0)
 
 
-@pytest.mark.parametrize("mode", ["table", "pair", "wide"])
+@pytest.mark.parametrize("mode", ["table", "pair", "wide", "word"])
 def test_forced_steppers_agree_on_c3(gpu_ctx, mode):
     """C3's regex through each stepper that can hold it (dgrep_set_stepper)."""
     import dgrep
