@@ -2723,13 +2723,21 @@ hipError_t occ_t(int* b) {
 // chunk sized to fill whole rounds exactly) 4.13: keep powers of two. The LDS
 // slots pack a line's chunk-relative start (<= C) and '\n' index (<= C) in 16
 // bits each, with a start of exactly C = 65,536 flagged in the lane's tail:
-// 64 KiB is the hard limit, reached by Sheng splits of >= 30 GiB (C5).
+// 64 KiB is the hard limit (the adaptive choice stops at kShengMaxChunk).
 // `dens_cap` (0 = none) is the largest chunk whose expected matching lines,
 // at the match density of the previous scan of this pattern, fill at most a
 // quarter of a lane's LDS slots: a denser pattern keeps smaller chunks instead
 // of sending many lanes through the overflow pass (C4 at 16 KiB: 0.8 % of the
 // lanes overflow and the pass costs 8 % of the scan; at 8 KiB 0.07 %).
-constexpr uint64_t kShengMaxChunk = kMaxLaneChunk;
+// The adaptive Sheng chunk stops at 32 KiB: 64 KiB chunks (what a >= 30 GiB
+// split would take) are parity-correct since r05 but measured no faster, C5 32
+// GiB same box: 0.670-0.671 at 64 KiB vs 0.672-0.674 at 32 KiB (the access
+// pattern's ceiling had predicted +2-3 %); dgrep_set_lane_chunk forces 64 KiB.
+#ifndef DGREP_SHENG_MAX_CHUNK
+#define DGREP_SHENG_MAX_CHUNK 32768
+#endif
+constexpr uint64_t kShengMaxChunk = DGREP_SHENG_MAX_CHUNK;
+static_assert(kShengMaxChunk <= uint64_t(kMaxLaneChunk), "adaptive chunk above the slot limit");
 // Per-stepper ceiling: the pair stepper stops at 8 KiB. Round 2 (static
 // tiles) measured 8 KiB 4.43 ms, 16 KiB 4.39, 32 KiB 4.71 per 16 GiB (at 32
 // KiB most of its ~40 records per lane and tile go through the HBM spill
