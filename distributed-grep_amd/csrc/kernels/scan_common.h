@@ -106,7 +106,7 @@ struct ScanArgs {
   // kStepPair only (byte offsets into the LDS image, see StepPair)
   uint32_t pair_t1;   // single-byte table T1
   uint32_t pair_thr;  // lowest premultiplied shadow state: a pair ending at >= thr holds an event
-  uint32_t pair_div;  // bytes per T2 row (2 * nclasses^2): premultiplied state / pair_div = state id
+  uint32_t pair_div;  // bytes per T2 row (esz * nclasses^2, padded): premultiplied state / pair_div = state id
   // kStepFilter only: the premultiplied CAND_END state (a '\n' ends a line that
   // left the LDS-resident part of the DFA: a candidate, verified afterwards)
   uint32_t cand_end;
@@ -272,6 +272,18 @@ constexpr uint32_t kPairMaxT2 = 32768;
 #ifndef DGREP_PAIR_U8
 #define DGREP_PAIR_U8 0
 #endif
+// StepPair's T2 entries are u32 (ds_read_b32) when the whole image fits
+// kPairW32MaxImage, else u16 (DGREP_PAIR_T2_U32=0: always u16). A u16 chain
+// value carried across the previous word's event branch is re-masked by one
+// v_and per word (LLVM keeps the phi as i16); a u32 entry has nothing to mask.
+#ifndef DGREP_PAIR_T2_U32
+#define DGREP_PAIR_T2_U32 1
+#endif
+static_assert(!(DGREP_PAIR_U8 && DGREP_PAIR_T2_U32), "u8 byte tables hold 2 class(b): u16 T2 only");
+constexpr uint32_t kPairW32MaxImage = 16384;
+// OR-ed into the stepper kind handed to the scan entry points (scan_dfa,
+// scan_tile_bytes, ...): the pair stepper's u32-entry build
+constexpr int kKindW32 = 0x100;
 constexpr uint32_t kPairMaxImage = 40960;
 constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the byte tables)
 // StepWord's LDS image (u32 entries, see StepWord): UA, UB [256] at 0 / 1024,

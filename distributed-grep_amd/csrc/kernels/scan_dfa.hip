@@ -310,8 +310,10 @@ struct StepWide {
 // pair-end state >= thr means an event -- at its first byte if it is a shadow
 // other than start_m, at its second byte if it is >= M (start_m or its shadow).
 
-struct StepPair {
+template <uint32_t ESZ>
+struct StepPairT {
   static constexpr int kKind = kStepPair;
+  static constexpr uint32_t kEsz = ESZ;  // bytes per T2 entry (u16 / u32)
   static constexpr uint32_t kBase = 0u;  // UA, UB, then T2 at kPairT2
   static constexpr uint32_t kT2 = kBase + kPairT2;
   const uint8_t* lds;
@@ -345,6 +347,7 @@ struct StepPair {
   }
   __device__ __forceinline__ Pre prep(uint32_t x) const { return prep_bytes(x); }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
+    if constexpr (ESZ == 4) return *reinterpret_cast<const uint32_t*>(lds + off);
     return *reinterpret_cast<const uint16_t*>(lds + off);
   }
   __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return t2(s + p.a0 + p.b1); }
@@ -369,7 +372,7 @@ struct StepPair {
   }
   // single-byte step (rare paths): state id = (premultiplied state - T2 base) / row bytes
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-    const uint32_t c = DGREP_PAIR_U8 ? uint32_t(lds[kBase + b]) >> 1 : ub(b) >> 1;
+    const uint32_t c = DGREP_PAIR_U8 ? uint32_t(lds[kBase + b]) >> 1 : ub(b) / ESZ;
     return T1[((s - kT2) / div) * K + c];
   }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
@@ -380,6 +383,11 @@ struct StepPair {
            (uint32_t(s3 >= M) << 3);
   }
 };
+// T2 entries: u32 when the image fits 16 KiB (a u16 chain value carried
+// across the previous word's event branch is re-masked by one v_and per word:
+// LLVM keeps the phi as i16), else u16 (twice the states per image)
+using StepPair = StepPairT<4>;
+using StepPair16 = StepPairT<2>;
 
 // DFA with few WORD FUNCTIONS: ONE dependent table lookup per 4-byte word.
 // A word's effect on the DFA is a function S -> S; for the regexes of the
@@ -511,10 +519,17 @@ template <>
 __device__ __forceinline__ StepFilter make_step<StepFilter>(const uint8_t* lds, const ScanArgs& a) {
   return StepFilter{lds, a.cand_end};
 }
+template <class P>
+__device__ __forceinline__ P make_pair_step(const uint8_t* lds, const ScanArgs& a) {
+  return P{lds, reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div, a.nclasses};
+}
 template <>
 __device__ __forceinline__ StepPair make_step<StepPair>(const uint8_t* lds, const ScanArgs& a) {
-  return StepPair{lds, reinterpret_cast<const uint16_t*>(lds + a.pair_t1), a.pair_thr, a.start_m, a.pair_div,
-                  a.nclasses};
+  return make_pair_step<StepPair>(lds, a);
+}
+template <>
+__device__ __forceinline__ StepPair16 make_step<StepPair16>(const uint8_t* lds, const ScanArgs& a) {
+  return make_pair_step<StepPair16>(lds, a);
 }
 
 template <>
@@ -554,8 +569,8 @@ struct Tune<StepFilter> {
   static constexpr int C = DGREP_FILTER_CHUNK, E = DGREP_FILTER_SLOTS, B = DGREP_FILTER_BLOCK, S = 1;
 };
 static_assert(Tune<StepFilter>::C % Tune<StepFilter>::B == 0 && Tune<StepFilter>::C <= 32768, "bad filter chunk");
-template <>
-struct Tune<StepPair> {
+template <uint32_t ESZ>
+struct Tune<StepPairT<ESZ>> {
   static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = DGREP_PAIR_STREAMS;
 };
 static_assert(Tune<StepPair>::B == 64 || Tune<StepPair>::B == 128, "block must be 64 or 128 bytes");
@@ -939,11 +954,25 @@ __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
   b.lnl = lnl_update<J>(b.lnl, m);
 }
 
+// Steppers whose per-word event test is a wave-uniform branch on the ballot
+// (v_cmp, s_cmp, s_cbranch_scc when no lane has an event) instead of an
+// exec-mask region (s_and_saveexec, s_cbranch_execnz, s_or_b64 exec on every
+// word). Bit k = stepper kind k.
+#ifndef DGREP_EV_BALLOT
+#define DGREP_EV_BALLOT 0
+#endif
 template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
-  if (__builtin_expect(word_any(st, M, s0, s1, s2, s3), 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+  const bool ev = word_any(st, M, s0, s1, s2, s3);
+  if constexpr (((DGREP_EV_BALLOT) >> Step::kKind) & 1) {
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
+      if (ev) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+    }
+  } else {
+    if (__builtin_expect(ev, 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+  }
   word_nl<J>(m, b);
 }
 
@@ -1369,6 +1398,16 @@ __device__ __forceinline__ void lazy_map(const Step& st, const uint8_t* p, uint2
   *mapsl = make_uint2(lo, hi);
 }
 
+// Steppers whose in-chunk blocks run in a separate wave-uniform loop (see
+// run_lane_from). Bit k = stepper kind k.
+#ifndef DGREP_UNIFORM_MAIN
+#define DGREP_UNIFORM_MAIN 0
+#endif
+template <class Step, bool DIRECT>
+constexpr bool uniform_main() {
+  return !DIRECT && (((DGREP_UNIFORM_MAIN) >> Step::kKind) & 1);
+}
+
 // Runs a lane (see file comment) from chunk-relative position pos0 over
 // BK-byte blocks with direct per-lane loads, prefetching the next block while
 // the current one is stepped (two register buffers, ping-pong). Returns the
@@ -1451,6 +1490,38 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   if (pos + BK > avail) {                                                                  \
     run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);                  \
     break;                                                                                 \
+  }
+  if constexpr (uniform_main<Step, DIRECT>()) {
+    // The blocks inside the chunk of a wave whose lanes all hold C + BK bytes:
+    // no lane leaves before C, so this loop's trip count is wave-uniform --
+    // scalar loop control, none of the per-lane exit masks (and their SALU
+    // merges at every latch) of the loop below, which then runs only past C.
+    if (pos < uint64_t(C) && __all(avail >= uint64_t(C) + BK)) {
+      do {
+        if constexpr (kMap && kLazyMapBytes != 0) {
+          if (maps && pos == kLazyMapBytes) {
+            if (r.nl != 0u)
+              *emit.cmap = make_uint4(0u, 0u, kLazyNewline, 0u);
+            else
+              lazy_map(st, p, emit.mapsl);
+          }
+        }
+        load_block<BK>(B, p + pos + BK);
+        DG_STEP(A, B)
+        pos += BK;
+        if constexpr (kMap && kLazyMapBytes != 0) {
+          if (maps && pos == kLazyMapBytes) {
+            if (r.nl != 0u)
+              *emit.cmap = make_uint4(0u, 0u, kLazyNewline, 0u);
+            else
+              lazy_map(st, p, emit.mapsl);
+          }
+        }
+        load_block<BK>(A, p + pos + BK);
+        DG_STEP(B, A)
+        pos += BK;
+      } while (pos < uint64_t(C));
+    }
   }
   for (;;) {
     DG_CHECK
@@ -2840,14 +2911,16 @@ hipError_t part_sheng(int, uint32_t, const Op& op) {
 }
 template <class Op>
 hipError_t part_pair(int kind, uint32_t table_bytes, const Op& op) {
-  if (kind == kStepWord) {
+  if ((kind & ~kKindW32) == kStepWord) {
     if (table_bytes <= 8192) return op.template run<StepWord, 8192>();
     return op.template run<StepWord, int(kWordMaxImage)>();
   }
-  if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
-  if (table_bytes <= 12288) return op.template run<StepPair, 12288>();  // C3 (9.5 KiB)
-  if (table_bytes <= 16384) return op.template run<StepPair, 16384>();
-  return op.template run<StepPair, int(kPairMaxImage)>();
+  if (kind & kKindW32) {
+    if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
+    return op.template run<StepPair, int(kPairW32MaxImage)>();  // C3 (15.6 KiB)
+  }
+  if (table_bytes <= 16384) return op.template run<StepPair16, 16384>();
+  return op.template run<StepPair16, int(kPairMaxImage)>();
 }
 template <class Op>
 hipError_t part_table(int, uint32_t table_bytes, const Op& op) {
@@ -2893,10 +2966,11 @@ DG_OPS(extern template, part_big)
 // One switch for every entry point: stepper by kind.
 template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, const Op& op) {
-  if (kind == kStepSheng8) return part_sheng(kind, table_bytes, op);
-  if (kind == kStepPair || kind == kStepWord) return part_pair(kind, table_bytes, op);
-  if (kind == kStepWide || kind == kStepFilter) return part_big(kind, table_bytes, op);
-  return part_table(kind, table_bytes, op);
+  const int k = kind & ~kKindW32;
+  if (k == kStepSheng8) return part_sheng(k, table_bytes, op);
+  if (k == kStepPair || k == kStepWord) return part_pair(kind, table_bytes, op);
+  if (k == kStepWide || k == kStepFilter) return part_big(k, table_bytes, op);
+  return part_table(k, table_bytes, op);
 }
 }  // namespace scan_ops
 
@@ -2910,7 +2984,8 @@ uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t re
   (void)dispatch(kind, table_bytes,
                  TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots, spill_per_lane});
   *threads = *waves_per_block * 64;
-  *spills = kind == kStepSheng8 || kind == kStepPair || kind == kStepFilter || kind == kStepWord;
+  const int k = kind & ~kKindW32;
+  *spills = k == kStepSheng8 || k == kStepPair || k == kStepFilter || k == kStepWord;
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {

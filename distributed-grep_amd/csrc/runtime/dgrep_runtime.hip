@@ -105,7 +105,7 @@ struct WordArgs {
   uint32_t W, P;
 };
 struct PairArgs {
-  uint32_t t1 = 0, thr = 0, div = 0;
+  uint32_t t1 = 0, thr = 0, div = 0, w32 = 0;
 };
 
 struct dgrep_ctx {
@@ -236,6 +236,12 @@ struct dgrep_ctx {
   uint64_t red_out_cap = 0;
 };
 
+// the kind handed to the scan entry points: the stepper, with kKindW32 for the
+// pair stepper's u32-entry image
+static int launch_kind(const dgrep_ctx* c) {
+  return c->step_kind | (c->step_kind == kStepPair && c->pair_args.w32 ? kKindW32 : 0);
+}
+
 namespace {
 
 int hip_fail(dgrep_ctx* c, hipError_t e, const char* what) {
@@ -260,7 +266,7 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 }
 
 // The pair stepper's LDS image (StepPair, scan_dfa.hip) from the blob's DFA:
-// UA, UB u32 [256] (byte -> column offsets), T2 u16 [S'][K][K] at kPairT2 (two
+// UA, UB u32 [256] (byte -> column offsets), T2 u32 (u16 if the image exceeds 16 KiB) [S'][K][K] at kPairT2 (two
 // bytes per lookup), T1 u16 [S'][K] (single bytes); states premultiplied to
 // their T2 row's LDS address (kPairT2 + id * 2K^2). S' = S + shadows: a pair whose FIRST byte is a '\n'
 // entering start_m hides that event in the state between its bytes, so it
@@ -284,11 +290,18 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
       if (std::find(targets.begin(), targets.end(), y) == targets.end()) targets.push_back(y);
     }
   const uint32_t Sp = S + uint32_t(targets.size());
-  // bytes per T2 row: 2K^2, padded to an ODD number of dwords so that the
-  // same column of different rows falls in different LDS banks
-  const uint64_t row = ((2ull * K * K + 3) & ~3ull) | 4ull;
+  // T2 entry: u32 when the image fits kPairW32MaxImage, else u16. Bytes per T2
+  // row: esz K^2, padded to an ODD number of dwords so that the same column of
+  // different rows falls in different LDS banks
+  auto row_of = [&](uint64_t esz) { return ((esz * K * K + 3) & ~3ull) | 4ull; };
+  auto end_of = [&](uint64_t r) {
+    const uint64_t t1 = (kPairT2 + r * Sp + 15) & ~15ull;
+    return std::make_pair(t1, (t1 + 2ull * Sp * K + 15) & ~15ull);
+  };
+  uint32_t esz = DGREP_PAIR_T2_U32 && end_of(row_of(4)).second <= kPairW32MaxImage ? 4u : 2u;
+  const uint64_t row = row_of(esz);
   if (row * Sp > kPairMaxT2) return false;
-  const uint64_t t1_off = (kPairT2 + row * Sp + 15) & ~15ull, end = (t1_off + 2ull * Sp * K + 15) & ~15ull;
+  const uint64_t t1_off = end_of(row).first, end = end_of(row).second;
   if (end > kPairMaxImage) return false;
   std::vector<uint32_t> id(S), orig(Sp);
   uint32_t next = 0;
@@ -306,7 +319,7 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   img->assign(end, 0);
   uint32_t* ua = reinterpret_cast<uint32_t*>(img->data());
   uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + 1024);
-  uint16_t* t2 = reinterpret_cast<uint16_t*>(img->data() + kPairT2);
+  uint8_t* const t2 = img->data() + kPairT2;
   uint16_t* t1 = reinterpret_cast<uint16_t*>(img->data() + t1_off);
   for (uint32_t i = 0; i < Sp; ++i) {
     const uint32_t x = orig[i];
@@ -316,14 +329,21 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
       t1[size_t(i) * K + c1] = premul(id[a]);
       for (uint32_t c2 = 0; c2 < K; ++c2) {
         const uint32_t y = T(a, c2);
-        t2[size_t(i) * (row / 2) + size_t(c1) * K + c2] = premul(flagged ? shadow_of[y] : id[y]);
+        const uint16_t v = premul(flagged ? shadow_of[y] : id[y]);
+        uint8_t* const e = t2 + size_t(i) * row + esz * (size_t(c1) * K + c2);
+        if (esz == 4) {
+          const uint32_t v32 = v;
+          memcpy(e, &v32, 4);
+        } else {
+          memcpy(e, &v, 2);
+        }
       }
     }
   }
   for (int b = 0; b < 256; ++b) {
     const uint32_t c = h.byte_class[b];
-    ua[b] = 2u * K * c;
-    ub[b] = 2u * c;
+    ua[b] = esz * K * c;
+    ub[b] = esz * c;
   }
   if (DGREP_PAIR_U8) {
     // one u8 table C[b] = 2 class(b) at LDS 0 (over UA); 2 (K - 1) < 256
@@ -336,6 +356,7 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   pa->t1 = uint32_t(t1_off);
   pa->thr = premul(thr_id);
   pa->div = uint32_t(row);
+  pa->w32 = esz == 4 ? 1u : 0u;
   return true;
 }
 
@@ -855,7 +876,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   }
   c->empty_line_matches = trans[size_t(h.start) * h.nclasses + h.byte_class[uint8_t('\n')]] == h.start_m;
   int bpc = 0;
-  HIPCHK(scan_dfa_occupancy(c->step_kind, c->table_bytes, &bpc));
+  HIPCHK(scan_dfa_occupancy(launch_kind(c), c->table_bytes, &bpc));
   c->blocks_per_cu = std::max(1, std::min(bpc, DGREP_MAX_WG_PER_CU));
   c->density = 0.0;
   c->staged_hint = 0;
@@ -1022,7 +1043,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   const uint64_t resident = uint64_t(c->num_cus) * uint64_t(c->blocks_per_cu);
   uint32_t chunk = 0, wpb = 1, slots = 0, threads = 0;
   bool spills = false;
-  const uint64_t tile = scan_tile_bytes(c->step_kind, c->table_bytes, n, resident, c->lane_chunk, c->density,
+  const uint64_t tile = scan_tile_bytes(launch_kind(c), c->table_bytes, n, resident, c->lane_chunk, c->density,
                                         DGREP_SPILL_RECORDS, &chunk, &wpb, &slots, &threads, &spills);
   const uint64_t ntiles = (n + tile - 1) / tile;
   int rc;
@@ -1152,7 +1173,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     a.epoch = c->epoch;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, kCounters * sizeof(unsigned long long), c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
-    HIPCHK(scan_dfa(c->step_kind, a, grid, c->stream));
+    HIPCHK(scan_dfa(launch_kind(c), a, grid, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     if (speculate && !in_scan)
       HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
@@ -1190,7 +1211,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   const bool over = ctr[1] && staged <= a.capacity;
   if (over) {
     HIPCHK(hipEventRecord(c->ev2, c->stream));
-    HIPCHK(scan_dfa_overflow(c->step_kind, a, ctr[1], c->stream));
+    HIPCHK(scan_dfa_overflow(launch_kind(c), a, ctr[1], c->stream));
     HIPCHK(hipEventRecord(c->ev3, c->stream));
   }
   uint64_t total = staged;
