@@ -730,6 +730,20 @@ struct Emitter {
     if (r.nev - uint32_t(E) < spill_cap) spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);  // wraps below E
     r.nev += own ? 1u : 0u;
   }
+  // inner_flat run by EVERY lane of the wave (word_events_wave): count = the
+  // lane has this record; the others write to an unclaimed slot. The spill
+  // store, rare, behind a ballot branch.
+  __device__ __forceinline__ void inner_wave(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool count) const {
+    const uint32_t lw = q - start;
+    const uint32_t w0 = start | (rel << 16);
+    const uint32_t i = min(r.nev, uint32_t(E));
+    *reinterpret_cast<uint2*>(slots + 2u * i) = make_uint2(w0, lw);
+    const bool sp = count && r.nev >= uint32_t(E);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(sp) != 0, 0)) {
+      if (sp && r.nev - uint32_t(E) < spill_cap) spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
+    }
+    r.nev += count ? 1u : 0u;
+  }
   __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
     const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
     if (DIRECT) {
@@ -899,6 +913,10 @@ __device__ __forceinline__ bool word_any(const Step& st, uint32_t M, uint32_t s0
 // are chunk-relative 32-bit values. Anything else (several '\n' in one word,
 // the part past the chunk end) takes the general loop.
 template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_emit_loop(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
+                                               uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
+                                               const Emitter<E, DIRECT>& emit);
+template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                           uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
                                           const Emitter<E, DIRECT>& emit) {
@@ -923,6 +941,14 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
       emit.inner(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, cand_of(st, sk));
     return;
   }
+  word_emit_loop<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+}
+
+// word_emit's general loop: several '\n' in the word, or past the chunk end
+template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_emit_loop(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
+                                               uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
+                                               const Emitter<E, DIRECT>& emit) {
   const uint64_t q0 = b.pos + 4u * J;
   const bool nl_w = b.lnl >= kLnlBase;  // a '\n' in an earlier word of this block
   const bool seen_w = sentinel<Step>() ? b.lnl != 0 : (r.seen || b.lnl != 0);
@@ -955,18 +981,48 @@ __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
 }
 
 // Steppers whose per-word event test is a wave-uniform branch on the ballot
-// (v_cmp, s_cmp, s_cbranch_scc when no lane has an event) instead of an
-// exec-mask region (s_and_saveexec, s_cbranch_execnz, s_or_b64 exec on every
-// word). Bit k = stepper kind k.
+// (v_cmp, s_cbranch_vccnz when no lane has an event) instead of an exec-mask
+// region (s_and_saveexec, s_cbranch_execnz, s_or_b64 exec on every word: pair
+// hot path 4.3 -> 2.4 SALU per word). Bit k = stepper kind k. Same-box A/B,
+// C3 kernel (with the uniform in-chunk loop): 0.581-0.584 -> 0.582-0.589; C4
+// (filter) 0.475-0.477 -> 0.470-0.484 (two runs +1.5 %, one -1 %); on the
+// Sheng stepper (round 3, before the pipelined pair chain) C2 lost 2 %.
 #ifndef DGREP_EV_BALLOT
-#define DGREP_EV_BALLOT 0
+#define DGREP_EV_BALLOT ((1 << kStepPair) | (1 << kStepFilter))
 #endif
+// The event fast path run by the whole wave once any lane has an event
+// (word_events, Emitter::inner_wave): selects instead of the nested exec-mask
+// regions of the single-'\n' test, the own test and the spill test. Needs
+// the flat emitter and the sentinel line start; no filter candidates.
+#ifndef DGREP_EV_WAVE
+#define DGREP_EV_WAVE 0
+#endif
+template <class Step, bool DIRECT>
+constexpr bool ev_wave() {
+  return flat_emit<Step, DIRECT>() && sentinel<Step>() && Step::kKind != kStepFilter && Step::kKind != kStepWord &&
+         (((DGREP_EV_WAVE) >> Step::kKind) & 1);
+}
 template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
   const bool ev = word_any(st, M, s0, s1, s2, s3);
-  if constexpr (((DGREP_EV_BALLOT) >> Step::kKind) & 1) {
+  if constexpr (ev_wave<Step, DIRECT>()) {
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
+      // the fast path by every lane, no exec-mask regions (see inner_wave):
+      // counted for an event word with one '\n', inside the chunk, owned
+      uint32_t t;
+      asm("v_ffbl_b32 %0, %1" : "=v"(t) : "v"(m));  // ffbl(0) = ~0: garbage for uncounted lanes
+      const uint32_t k = t >> 3;
+      const bool single = (m & (m - 1u)) == 0u;
+      const uint32_t start = uint32_t(b.pos) + (b.lnl >> 3) - (2u + kLnlOff);
+      emit.inner_wave(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, ev && single && !b.past && b.lnl != 0);
+      const bool gen = ev && !(single && !b.past);
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(gen) != 0, 0)) {
+        if (gen) word_emit_loop<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+      }
+    }
+  } else if constexpr (((DGREP_EV_BALLOT) >> Step::kKind) & 1) {
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
       if (ev) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
     }
@@ -1399,9 +1455,12 @@ __device__ __forceinline__ void lazy_map(const Step& st, const uint8_t* p, uint2
 }
 
 // Steppers whose in-chunk blocks run in a separate wave-uniform loop (see
-// run_lane_from). Bit k = stepper kind k.
+// run_lane_from). Bit k = stepper kind k. Same-box A/B (profiles/r05/ablation/
+// uniform_main.txt): C3 kernel 0.577-0.579 -> 0.581-0.584 (the latch's ~100
+// SALU of exit-mask merges per two blocks gone); C2 (Sheng) unchanged, C4
+// (filter) 0.479-0.485 -> 0.475-0.476, so pair only.
 #ifndef DGREP_UNIFORM_MAIN
-#define DGREP_UNIFORM_MAIN 0
+#define DGREP_UNIFORM_MAIN (1 << kStepPair)
 #endif
 template <class Step, bool DIRECT>
 constexpr bool uniform_main() {
