@@ -190,7 +190,18 @@ struct LongDfaArgs {
   const uint64_t* seg_off;  // [npend + 1]
   PendingLine* pend;
   uint64_t npend;
+  // long_dfa_seg_kernel's LDS copy of a u16 DFA (xrec != nullptr): the first
+  // x_hot rows whole, then one DfaXRec for each of the next x_rec states (the
+  // rest read from `full`)
+  const uint2* xrec;
+  uint32_t x_hot, x_rec;
 };
+// A state past the LDS-resident rows whose row equals the row of a resident
+// DEFAULT state except in at most two classes (keyword automata: 4,608 of
+// config 4's 4,978 such states differ in one class, 367 in two, 2 in three):
+// x = default id (0xffff: none, read `full`) | class 1 << 16 | class 2 << 24
+// (0xff: unused), y = next state on class 1 | next state on class 2 << 16.
+constexpr uint32_t kXNone = 0xffu;
 
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids
 struct VerifyArgs {
@@ -215,6 +226,11 @@ struct VerifyArgs {
   // resolved pending long lines (StagedLine kMetaPend: len_lo = index)
   const PendingLine* pend;
   uint32_t nfa_words;  // the NFA program's position-set words (nw)
+  // u16 DFAs: the rows + DfaXRec LDS copy (see LongDfaArgs); nullptr: the
+  // first hot_entries of `full` only
+  const uint2* xrec;
+  uint32_t x_hot, x_rec;
+  uint32_t num_cus;
 };
 
 // LDS slot records (8 B: start16 | rel16, then w1): w1 = the line's length with

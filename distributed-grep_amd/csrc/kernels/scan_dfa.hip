@@ -2084,6 +2084,43 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
 // are the first ones: kVerifyHotBytes of them are copied to LDS, the rest are
 // read from HBM (L2-resident: [state][class], u16 entries, or u32 above 65535
 // states). A line is read in aligned 16-byte pieces.
+// The whole DFA (breadth-first ids, [state][class]) as the verification and
+// long-line kernels read it: rows [0, hot_n / K) in LDS, optionally DfaXRec
+// records for the next xn states (LDS), the rest from HBM (L2-resident).
+template <typename E>
+struct FullDfa {
+  const E* hot;  // LDS
+  const __attribute__((address_space(1))) E* full;
+  const uint32_t* cls;  // LDS
+  uint32_t K, hot_n;
+  const uint2* xr = nullptr;  // LDS: DfaXRec of states [hot_n / K, + xn) (see LongDfaArgs)
+  uint32_t xh = 0, xn = 0;
+  __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t b) const { return next_cls(s, cls[b]); }
+  __device__ __forceinline__ uint32_t next_cls(uint32_t s, uint32_t c) const {
+    const size_t i = size_t(s) * K + c;
+    if (i < hot_n) return uint32_t(hot[i]);
+    if (xr != nullptr && s - xh < xn) {
+      // the default row's entry unless this class is one of the exceptions
+      const uint2 r = xr[s - xh];
+      if (c == ((r.x >> 16) & 0xffu)) return r.y & 0xffffu;
+      if (c == (r.x >> 24)) return r.y >> 16;
+      const uint32_t d = r.x & 0xffffu;
+      if (d != 0xffffu) return uint32_t(hot[d * K + c]);
+    }
+    return uint32_t(full[i]);
+  }
+  // state after bytes [a, e) from s, stopping at the absorbing `matched`
+  __device__ __forceinline__ uint32_t run(const uint8_t* data, uint64_t a, uint64_t e, uint32_t s,
+                                          uint32_t matched) const {
+    if (s == matched) return s;
+    for_line_bytes(data, a, e, [&](uint32_t b) {
+      s = next(s, b);
+      return s != matched;
+    });
+    return s;
+  }
+};
+
 constexpr uint32_t kVerifyHotBytes = 48 * 1024;
 constexpr uint32_t kVerifyLookback = 256;  // bytes a wave-verified segment's entry state is guessed from
 
@@ -2099,9 +2136,9 @@ struct NoWavePred {
 template <class Pred, class WavePred = NoWavePred>
 __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_matches, WavePred&& wave_matches = {}) {
   constexpr bool kWave = !std::is_same<std::decay_t<WavePred>, NoWavePred>::value;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t waves = uint64_t(gridDim.x) * 4;
-  for (uint64_t t = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
+  const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x / 64u;
+  const uint64_t waves = uint64_t(gridDim.x) * wpb;
+  for (uint64_t t = uint64_t(blockIdx.x) * wpb + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
     const TileInfo ti = v.tiles[t];
     if (ti.count == 0) continue;
     uint32_t kept = 0;
@@ -2152,21 +2189,33 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
   }
 }
 
-template <typename E>
-__global__ __launch_bounds__(256) void verify_kernel(VerifyArgs v) {
+// XR: the DFA's rows and default-row records (DfaXRec, as long_dfa_seg_kernel)
+// in one 1024-thread workgroup's LDS, one resident workgroup per CU; else the
+// first kVerifyHotBytes of rows in each 256-thread workgroup's LDS
+template <typename E, bool XR>
+__global__ __launch_bounds__(XR ? 1024 : 256) void verify_kernel(VerifyArgs v) {
+  constexpr uint32_t NT = XR ? 1024 : 256;
+  constexpr uint32_t kLds = XR ? 158u * 1024u : kVerifyHotBytes;
   __shared__ uint32_t cls[256];
-  __shared__ __attribute__((aligned(16))) E hot[kVerifyHotBytes / sizeof(E)];
-  cls[threadIdx.x] = v.cls[threadIdx.x];
+  __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLds];
+  if (threadIdx.x < 256) cls[threadIdx.x] = v.cls[threadIdx.x];
+  E* const hot = reinterpret_cast<E*>(lbuf);
   const E* full = static_cast<const E*>(v.full);
-  const uint32_t hot_n = v.hot_entries;
-  for (uint32_t i = threadIdx.x; i < hot_n; i += 256) hot[i] = full[i];
+  const uint32_t hot_n = XR ? v.x_hot * v.nclasses : v.hot_entries;
+  for (uint32_t i = threadIdx.x; i < hot_n; i += NT) hot[i] = full[i];
+  uint2* const xr = reinterpret_cast<uint2*>(lbuf + ((hot_n * sizeof(E) + 7u) & ~7u));
+  if constexpr (XR)
+    for (uint32_t i = threadIdx.x; i < v.x_rec; i += NT) xr[i] = v.xrec[i];
   __syncthreads();
   const __attribute__((address_space(1))) E* gfull = (const __attribute__((address_space(1))) E*)v.full;
   const uint32_t K = v.nclasses, cn = cls['\n'];
-  auto next = [&](uint32_t s, uint32_t c) -> uint32_t {
-    const size_t i = size_t(s) * K + c;
-    return i < hot_n ? uint32_t(hot[i]) : uint32_t(gfull[i]);
-  };
+  FullDfa<E> d{hot, gfull, cls, K, hot_n};
+  if constexpr (XR) {
+    d.xr = xr;
+    d.xh = v.x_hot;
+    d.xn = v.x_rec;
+  }
+  auto next = [&](uint32_t s, uint32_t c) -> uint32_t { return d.next_cls(s, c); };
   // state after [a, e) from s, stopping at the absorbing MATCHED state
   auto run = [&](uint64_t a, uint64_t e, uint32_t s) -> uint32_t {
     if (s == v.matched) return s;
@@ -2619,44 +2668,34 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
 // segment from the true state when it was not (exact for any DFA).
 constexpr uint32_t kLongLookback = 256;
 
-template <typename E>
-struct FullDfa {
-  const E* hot;  // LDS
-  const __attribute__((address_space(1))) E* full;
-  const uint32_t* cls;  // LDS
-  uint32_t K, hot_n;
-  __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t b) const {
-    const size_t i = size_t(s) * K + cls[b];
-    return i < hot_n ? uint32_t(hot[i]) : uint32_t(full[i]);
-  }
-  // state after bytes [a, e) from s, stopping at the absorbing `matched`
-  __device__ __forceinline__ uint32_t run(const uint8_t* data, uint64_t a, uint64_t e, uint32_t s,
-                                          uint32_t matched) const {
-    if (s == matched) return s;
-    for_line_bytes(data, a, e, [&](uint32_t b) {
-      s = next(s, b);
-      return s != matched;
-    });
-    return s;
-  }
-};
 
 // one 1024-thread workgroup per CU holds the DFA's first kLongDfaHotBytes of
 // rows (breadth-first: the states keyword text spends its bytes in; C4's
 // depth <= 3 rows need ~110 KiB) -- the segment lanes' table reads stay in LDS
 constexpr int kLongDfaThreads = 1024;
-constexpr uint32_t kLongDfaHotBytes = 120 * 1024;
+constexpr uint32_t kLongDfaHotBytes = 120 * 1024;  // rows alone (u32 DFAs)
+constexpr uint32_t kLongDfaLdsBytes = 158 * 1024;  // rows + DfaXRec (u16 DFAs)
 
 template <typename E>
 __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg_kernel(LongDfaArgs la) {
   __shared__ uint32_t cls[256];
-  __shared__ __attribute__((aligned(16))) E hot[kLongDfaHotBytes / sizeof(E)];
+  __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLongDfaLdsBytes];
   if (threadIdx.x < 256) cls[threadIdx.x] = la.cls[threadIdx.x];
+  E* const hot = reinterpret_cast<E*>(lbuf);
   const E* full = static_cast<const E*>(la.full);
-  const uint32_t hot_n = min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
+  const bool xd = sizeof(E) == 2 && la.xrec != nullptr;
+  const uint32_t hot_n = xd ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
   for (uint32_t i = threadIdx.x; i < hot_n; i += kLongDfaThreads) hot[i] = full[i];
+  uint2* const xr = reinterpret_cast<uint2*>(lbuf + ((hot_n * sizeof(E) + 7u) & ~7u));
+  const uint32_t xn = xd ? la.x_rec : 0u;
+  for (uint32_t i = threadIdx.x; i < xn; i += kLongDfaThreads) xr[i] = la.xrec[i];
   __syncthreads();
-  const FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, hot_n};
+  FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, hot_n};
+  if (xd) {
+    d.xr = xr;
+    d.xh = la.x_hot;
+    d.xn = xn;
+  }
   // two segments per lane (g and g + half), stepped byte by byte in lockstep:
   // the chain is a dependent table read per byte, so two chains per lane
   // overlap their latencies. Each runs [lookback start, end) from `start`
@@ -3101,6 +3140,7 @@ hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream) {
 
 uint32_t long_lookback() { return kLongLookback; }
 uint32_t long_dfa_hot_bytes() { return kLongDfaHotBytes; }
+uint32_t long_dfa_lds_bytes() { return kLongDfaLdsBytes; }
 
 hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
   if (la.nseg) {
@@ -3133,9 +3173,13 @@ hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t s
   else if (v.nfa)
     hipLaunchKernelGGL(verify_nfa_kernel<kNfaMaxWords>, dim3(grid), dim3(256), 0, stream, v);
   else if (v.full_u32)
-    hipLaunchKernelGGL(verify_kernel<uint32_t>, dim3(grid), dim3(256), 0, stream, v);
+    hipLaunchKernelGGL((verify_kernel<uint32_t, false>), dim3(grid), dim3(256), 0, stream, v);
+  else if (v.xrec)
+    // one persistent 1024-thread workgroup per CU: the LDS copy once per CU
+    hipLaunchKernelGGL((verify_kernel<uint16_t, true>), dim3(std::min<uint64_t>(v.num_cus, (v.ntiles + 15) / 16)),
+                       dim3(1024), 0, stream, v);
   else
-    hipLaunchKernelGGL(verify_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, v);
+    hipLaunchKernelGGL((verify_kernel<uint16_t, false>), dim3(grid), dim3(256), 0, stream, v);
   return hipGetLastError();
 }
 

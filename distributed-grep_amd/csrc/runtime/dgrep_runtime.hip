@@ -91,6 +91,7 @@ hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream);
 hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream);
 uint32_t long_lookback();
 uint32_t long_dfa_hot_bytes();
+uint32_t long_dfa_lds_bytes();
 uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
@@ -139,6 +140,8 @@ struct dgrep_ctx {
   uint32_t blob_start = 0, blob_start_m = 0;  // start / start_m in d_full's (breadth-first) ids
   uint32_t blob_matched = UINT32_MAX;          // the absorbing accepting state in d_full's ids (none: UINT32_MAX)
   uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
+  uint2* d_xrec = nullptr;                     // long_dfa_seg_kernel's DfaXRec (u16 DFAs; see LongDfaArgs)
+  uint32_t x_hot = 0, x_rec = 0;
   uint32_t* d_nfa = nullptr;                   // DGREP_DFA_PARTIAL: the NFA program (verify_nfa_kernel)
   uint32_t nfa_words = 0;                      // its position-set words
   int blocks_per_cu = 1;
@@ -199,6 +202,8 @@ struct dgrep_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr;
   uint64_t staged_hint = 0;  // kStepFilter: staged lines (candidates included) of the last scan
   float last_ms = 0.f;
+  double ms_sum = 0.0;  // last_ms summed over the dgrep_scan_device calls since dgrep_take_kernel_ms
+  uint64_t ms_scans = 0;
   dgrep_scan_stats stats{};
   // matching lines per byte of the last scan of the loaded pattern (0 after
   // dgrep_load_dfa): caps the adaptive lane chunk (scan_tile_bytes)
@@ -263,6 +268,55 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
   HIPCHK(hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)));
   *cap = n;
   return DGREP_OK;
+}
+
+// long_dfa_seg_kernel's LDS copy of a u16 DFA F ([S][K], breadth-first ids):
+// the first *hot rows whole, then a DfaXRec (scan_common.h) for each of the
+// next states while the LDS budget lasts -- its default = the resident row
+// differing from its own in the fewest classes (exhaustive, stopping at one
+// difference; config 4: 4,978 records, 30 ms), exceptions <= 2, else no
+// default. The rows get what the records leave: all S states covered when
+// 8 S fits beside at least 64 rows, else half the budget each.
+#ifndef DGREP_LONG_XREC
+#define DGREP_LONG_XREC 1
+#endif
+// verify_kernel on the same LDS copy (one 1024-thread workgroup per CU)
+#ifndef DGREP_VERIFY_XREC
+#define DGREP_VERIFY_XREC 1
+#endif
+static void build_xrec(const uint16_t* F, uint32_t S, uint32_t K, uint32_t budget, uint32_t* hot,
+                       std::vector<uint2>* out) {
+  out->clear();
+  const uint64_t row = 2ull * K, B = budget - 8;  // 8: the records' alignment
+  uint64_t H = 0, R = 0;
+  if (B > 8ull * S && (B - 8ull * S) / (row - 8) >= 64) {
+    H = std::min<uint64_t>(S, (B - 8ull * S) / (row - 8));
+    R = S - H;
+  } else {
+    H = std::min<uint64_t>(S, B / 2 / row);
+    R = std::min<uint64_t>(S - H, (B - H * row) / 8);
+  }
+  *hot = uint32_t(H);
+  out->resize(R);
+  for (uint64_t j = 0; j < R; ++j) {
+    const uint16_t* f = F + (H + j) * K;
+    uint32_t best = 3, bd = 0xffffu;
+    for (uint64_t d = 0; d < H && best > 1; ++d) {
+      const uint16_t* g = F + d * K;
+      uint32_t diff = 0;
+      for (uint32_t k = 0; k < K && diff < best; ++k) diff += f[k] != g[k];
+      if (diff < best) { best = diff; bd = uint32_t(d); }
+    }
+    uint2 r = make_uint2(0xffffu | (kXNone << 16) | (kXNone << 24), 0u);
+    if (bd != 0xffffu) {
+      uint32_t cl[2] = {kXNone, kXNone}, nx[2] = {0, 0}, e = 0;
+      const uint16_t* g = F + uint64_t(bd) * K;
+      for (uint32_t k = 0; k < K; ++k)
+        if (f[k] != g[k]) { cl[e] = k; nx[e] = f[k]; ++e; }
+      r = make_uint2(bd | (cl[0] << 16) | (cl[1] << 24), nx[0] | (nx[1] << 16));
+    }
+    (*out)[j] = r;
+  }
 }
 
 // The pair stepper's LDS image (StepPair, scan_dfa.hip) from the blob's DFA:
@@ -594,7 +648,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_xrec, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
                   c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_seg_from, c->d_seg_state, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_order, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
@@ -720,6 +774,9 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_nfa = nullptr;
   if (c->d_full) HIPCHK(hipFree(c->d_full));
   c->d_full = nullptr;
+  if (c->d_xrec) HIPCHK(hipFree(c->d_xrec));
+  c->d_xrec = nullptr;
+  c->x_hot = c->x_rec = 0;
   if (pair_ok || word_ok) {
     // image built above
   } else if (filter_ok && partial) {
@@ -759,6 +816,15 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     HIPCHK(hipMalloc(&c->d_full, full.size()));
     HIPCHK(hipMemcpy(c->d_full, full.data(), full.size(), hipMemcpyHostToDevice));
     c->verify_hot = uint32_t(std::min<size_t>(ne, verify_hot_bytes() / esz)) / K * K;
+    if (!c->full_u32 && K < kXNone) {
+      std::vector<uint2> xr;
+      build_xrec(reinterpret_cast<const uint16_t*>(full.data()), S, K, long_dfa_lds_bytes(), &c->x_hot, &xr);
+      c->x_rec = uint32_t(xr.size());
+      if (!xr.empty()) {
+        HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_xrec), xr.size() * sizeof(uint2)));
+        HIPCHK(hipMemcpy(c->d_xrec, xr.data(), xr.size() * sizeof(uint2), hipMemcpyHostToDevice));
+      }
+    }
     if (!c->d_cls) HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_cls), 256));
     HIPCHK(hipMemcpy(c->d_cls, h.byte_class, 256, hipMemcpyHostToDevice));
     c->blob_start = bid[h.start];
@@ -1006,6 +1072,9 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   la.seg_off = c->d_seg_off;
   la.pend = c->d_pend;
   la.npend = npend;
+  la.xrec = DGREP_LONG_XREC ? c->d_xrec : nullptr;
+  la.x_hot = c->x_hot;
+  la.x_rec = c->x_rec;
   HIPCHK(long_lines_dfa(la, c->full_u32, c->stream));
   // the host vectors are read by the async copies above: wait before they go
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -1219,6 +1288,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   const bool verify = filt || npend;
   if (verify && staged && staged <= a.capacity) {
     VerifyArgs v;
+    memset(&v, 0, sizeof v);
     v.data = d_data;
     v.full = c->d_full;
     v.full_u32 = c->full_u32 ? 1u : 0u;
@@ -1236,6 +1306,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.nfa_words = c->nfa_words;
     v.matched = c->d_nfa ? UINT32_MAX : c->blob_matched;
     v.pend = c->d_pend;
+    v.xrec = DGREP_VERIFY_XREC ? c->d_xrec : nullptr;
+    v.x_hot = c->x_hot;
+    v.x_rec = c->x_rec;
+    v.num_cus = uint32_t(c->num_cus);
     HIPCHK(hipEventRecord(c->ev4, c->stream));
     if (npend && park_maps) {
       LongArgs la;
@@ -1325,7 +1399,12 @@ extern "C" int dgrep_scan_device(dgrep_ctx* c, const void* d_data, size_t n, uin
   if (!c || !count || (n && !d_data)) return DGREP_E_INVALID;
   if (!c->loaded) { c->err = "no DFA loaded"; return DGREP_E_NO_DFA; }
   HIPCHK(hipSetDevice(c->device));
-  return scan_resident(c, static_cast<const uint8_t*>(d_data), n, d_line_no, d_start, d_len, capacity, count);
+  const int rc = scan_resident(c, static_cast<const uint8_t*>(d_data), n, d_line_no, d_start, d_len, capacity, count);
+  if (rc == DGREP_OK) {
+    c->ms_sum += c->last_ms;
+    ++c->ms_scans;
+  }
+  return rc;
 }
 
 // Worker-side ingest of one split (the bytes map_reduce/worker.go:72-76
@@ -1641,6 +1720,15 @@ extern "C" void dgrep_result_free(dgrep_result* r) {
 extern "C" int dgrep_last_kernel_ms(dgrep_ctx* c, float* ms) {
   if (!c || !ms) return DGREP_E_INVALID;
   *ms = c->last_ms;
+  return DGREP_OK;
+}
+
+extern "C" int dgrep_take_kernel_ms(dgrep_ctx* c, double* sum_ms, uint64_t* scans) {
+  if (!c || !sum_ms || !scans) return DGREP_E_INVALID;
+  *sum_ms = c->ms_sum;
+  *scans = c->ms_scans;
+  c->ms_sum = 0.0;
+  c->ms_scans = 0;
   return DGREP_OK;
 }
 

@@ -52,7 +52,7 @@ EXPORTS = (
     "dgrep_compile", "dgrep_compile_budget", "dgrep_blob_free", "dgrep_blob_info_get", "dgrep_open", "dgrep_close",
     "dgrep_last_error", "dgrep_pick_device", "dgrep_set_stream", "dgrep_load_dfa", "dgrep_scan", "dgrep_result_free",
     "dgrep_scan_device", "dgrep_synth_corpus", "dgrep_synth_corpus_host", "dgrep_synth_keyword",
-    "dgrep_last_kernel_ms", "dgrep_set_stepper", "dgrep_set_lane_chunk", "dgrep_set_ingest", "dgrep_last_ingest_ms",
+    "dgrep_last_kernel_ms", "dgrep_take_kernel_ms", "dgrep_set_stepper", "dgrep_set_lane_chunk", "dgrep_set_ingest", "dgrep_last_ingest_ms",
     "dgrep_map_partitions", "dgrep_partitions_free", "dgrep_encode_device", "dgrep_last_encode_ms",
     "dgrep_reduce", "dgrep_reduce_free", "dgrep_last_scan_stats", "dgrep_build_info",
     "dgrep_comm_unique_id", "dgrep_comm_open", "dgrep_comm_close", "dgrep_gather_records_device",
@@ -160,6 +160,8 @@ def lib() -> ctypes.CDLL:
             L.dgrep_synth_keyword.restype = i
             L.dgrep_last_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
             L.dgrep_last_kernel_ms.restype = i
+            L.dgrep_take_kernel_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+            L.dgrep_take_kernel_ms.restype = i
             L.dgrep_set_ingest.argtypes = [vp, sz, i, i]
             L.dgrep_set_ingest.restype = i
             L.dgrep_last_ingest_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
@@ -406,6 +408,12 @@ class Context:
         ms = ctypes.c_float()
         self._check(self._L.dgrep_last_kernel_ms(self._h, ctypes.byref(ms)))
         return float(ms.value)
+
+    def take_kernel_ms(self):
+        """(sum of the scans' device ms, number of scans) since the previous take (dgrep_take_kernel_ms)."""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        self._check(self._L.dgrep_take_kernel_ms(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return float(ms.value), int(n.value)
 
     def scan_stats(self) -> dict:
         """dgrep_last_scan_stats of the last scan (stepper, lane chunk, overflow lanes, times)."""

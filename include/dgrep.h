@@ -263,6 +263,10 @@ int dgrep_synth_keyword(uint64_t seed, int i, char* out16);
  * (every attempt, if the overflow list had to grow) plus the overflow pass,
  * measured with HIP events on the launch stream. */
 int dgrep_last_kernel_ms(dgrep_ctx* ctx, float* ms);
+/* dgrep_last_kernel_ms summed over the dgrep_scan_device calls since the
+ * previous take (and their number), then reset: a benchmark reads its timed
+ * steps' device time once, after them, with no host call between scans. */
+int dgrep_take_kernel_ms(dgrep_ctx* ctx, double* sum_ms, uint64_t* scans);
 
 /* What the last dgrep_scan* call did (tests, tuning, bench reports). */
 typedef struct {
