@@ -190,17 +190,17 @@ struct LongDfaArgs {
   const uint64_t* seg_off;  // [npend + 1]
   PendingLine* pend;
   uint64_t npend;
-  // long_dfa_seg_kernel's LDS copy of a u16 DFA (xrec != nullptr): the first
-  // x_hot rows whole, then one DfaXRec for each of the next x_rec states (the
-  // rest read from `full`)
-  const uint2* xrec;
-  uint32_t x_hot, x_rec;
+  // the whole-DFA LDS image of a u16 DFA (runtime build_ximg; nullptr: the
+  // first rows in LDS, the rest read from `full`): x_hot rows (plus extra
+  // rows), then a DfaXRec per state >= x_hot at byte xr_off
+  const uint8_t* ximg;
+  uint32_t ximg_bytes, x_hot, xr_off;
 };
-// A state past the LDS-resident rows whose row equals the row of a resident
+// DfaXRec: a state past the LDS image's first rows reads the row of a resident
 // DEFAULT state except in at most two classes (keyword automata: 4,608 of
-// config 4's 4,978 such states differ in one class, 367 in two, 2 in three):
-// x = default id (0xffff: none, read `full`) | class 1 << 16 | class 2 << 24
-// (0xff: unused), y = next state on class 1 | next state on class 2 << 16.
+// config 4's 4,978 such states differ in one class, 367 in two; the 2 left
+// get an extra row of their own as default): x = default row | class 1 << 16
+// | class 2 << 24 (0xff: unused), y = next state on class 1 | on class 2 << 16.
 constexpr uint32_t kXNone = 0xffu;
 
 // verify_kernel's arguments (kStepFilter): the whole DFA with the blob's ids
@@ -226,10 +226,10 @@ struct VerifyArgs {
   // resolved pending long lines (StagedLine kMetaPend: len_lo = index)
   const PendingLine* pend;
   uint32_t nfa_words;  // the NFA program's position-set words (nw)
-  // u16 DFAs: the rows + DfaXRec LDS copy (see LongDfaArgs); nullptr: the
-  // first hot_entries of `full` only
-  const uint2* xrec;
-  uint32_t x_hot, x_rec;
+  // u16 DFAs: the whole-DFA LDS image (see LongDfaArgs); nullptr: the first
+  // hot_entries of `full` in LDS, the rest from HBM
+  const uint8_t* ximg;
+  uint32_t ximg_bytes, x_hot, xr_off;
   uint32_t num_cus;
 };
 

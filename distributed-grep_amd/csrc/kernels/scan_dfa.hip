@@ -2087,27 +2087,52 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
 // The whole DFA (breadth-first ids, [state][class]) as the verification and
 // long-line kernels read it: rows [0, hot_n / K) in LDS, optionally DfaXRec
 // records for the next xn states (LDS), the rest from HBM (L2-resident).
-template <typename E>
+template <typename E, bool XI = false>
 struct FullDfa {
   const E* hot;  // LDS
   const __attribute__((address_space(1))) E* full;
   const uint32_t* cls;  // LDS
-  uint32_t K, hot_n;
-  const uint2* xr = nullptr;  // LDS: DfaXRec of states [hot_n / K, + xn) (see LongDfaArgs)
-  uint32_t xh = 0, xn = 0;
+  uint32_t K, hot_n;    // hot_n = (resident rows) * K >= K
+  // XI (the whole-DFA LDS image, runtime build_ximg): the DfaXRec of state
+  // s >= xh at xr[s - xh]; its default row (a resident or an extra row) in hot
+  const uint2* xr = nullptr;
+  uint32_t xh = 0;
+  // 32-bit index math: s * K + c < 2^21 * 256 (the compiler's state budget)
   __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t b) const { return next_cls(s, cls[b]); }
   __device__ __forceinline__ uint32_t next_cls(uint32_t s, uint32_t c) const {
-    const size_t i = size_t(s) * K + c;
+    const uint32_t i = __umul24(s, K) + c;
     if (i < hot_n) return uint32_t(hot[i]);
-    if (xr != nullptr && s - xh < xn) {
-      // the default row's entry unless this class is one of the exceptions
-      const uint2 r = xr[s - xh];
-      if (c == ((r.x >> 16) & 0xffu)) return r.y & 0xffffu;
-      if (c == (r.x >> 24)) return r.y >> 16;
-      const uint32_t d = r.x & 0xffffu;
-      if (d != 0xffffu) return uint32_t(hot[d * K + c]);
+    return cold(s, c, i);
+  }
+  // two chains at once (long_dfa_seg_kernel): both resident-row reads issued
+  // unconditionally (clamped), the cold path entered only when a lane of the
+  // wave needs it
+  __device__ __forceinline__ void next2(uint32_t& sa, uint32_t ba, uint32_t& sb, uint32_t bb) const {
+    const uint32_t ca = cls[ba], cb = cls[bb];
+    const uint32_t ia = __umul24(sa, K) + ca, ib = __umul24(sb, K) + cb;
+    uint32_t na = uint32_t(hot[min(ia, hot_n - 1u)]), nb = uint32_t(hot[min(ib, hot_n - 1u)]);
+    const bool ka = ia >= hot_n, kb = ib >= hot_n;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(ka || kb) != 0, 0)) {
+      if (ka) na = cold(sa, ca, ia);
+      if (kb) nb = cold(sb, cb, ib);
     }
-    return uint32_t(full[i]);
+    sa = na;
+    sb = nb;
+  }
+  // a state past the resident rows: XI, its record (straight-line: the default
+  // row's entry read unconditionally, then the exceptions selected) -- no HBM
+  // read, so no vmcnt wait on the chain (a possible HBM result here made every
+  // step wait for the segment's data prefetch); else the HBM table
+  __device__ __forceinline__ uint32_t cold(uint32_t s, uint32_t c, uint32_t i) const {
+    if constexpr (XI) {
+      const uint2 r = xr[s - xh];
+      uint32_t t = uint32_t(hot[__umul24(r.x & 0xffffu, K) + c]);
+      t = c == (r.x >> 24) ? (r.y >> 16) : t;
+      t = c == ((r.x >> 16) & 0xffu) ? (r.y & 0xffffu) : t;
+      return t;
+    } else {
+      return uint32_t(full[i]);
+    }
   }
   // state after bytes [a, e) from s, stopping at the absorbing `matched`
   __device__ __forceinline__ uint32_t run(const uint8_t* data, uint64_t a, uint64_t e, uint32_t s,
@@ -2189,9 +2214,9 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
   }
 }
 
-// XR: the DFA's rows and default-row records (DfaXRec, as long_dfa_seg_kernel)
-// in one 1024-thread workgroup's LDS, one resident workgroup per CU; else the
-// first kVerifyHotBytes of rows in each 256-thread workgroup's LDS
+// XR: the whole-DFA LDS image (runtime build_ximg) in one 1024-thread
+// workgroup's LDS, one resident workgroup per CU; else the first
+// kVerifyHotBytes of rows in each 256-thread workgroup's LDS, the rest in HBM
 template <typename E, bool XR>
 __global__ __launch_bounds__(XR ? 1024 : 256) void verify_kernel(VerifyArgs v) {
   constexpr uint32_t NT = XR ? 1024 : 256;
@@ -2200,20 +2225,21 @@ __global__ __launch_bounds__(XR ? 1024 : 256) void verify_kernel(VerifyArgs v) {
   __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLds];
   if (threadIdx.x < 256) cls[threadIdx.x] = v.cls[threadIdx.x];
   E* const hot = reinterpret_cast<E*>(lbuf);
-  const E* full = static_cast<const E*>(v.full);
   const uint32_t hot_n = XR ? v.x_hot * v.nclasses : v.hot_entries;
-  for (uint32_t i = threadIdx.x; i < hot_n; i += NT) hot[i] = full[i];
-  uint2* const xr = reinterpret_cast<uint2*>(lbuf + ((hot_n * sizeof(E) + 7u) & ~7u));
-  if constexpr (XR)
-    for (uint32_t i = threadIdx.x; i < v.x_rec; i += NT) xr[i] = v.xrec[i];
+  if constexpr (XR) {
+    for (uint32_t i = threadIdx.x * 16u; i < v.ximg_bytes; i += NT * 16u)
+      *reinterpret_cast<uint4*>(lbuf + i) = *reinterpret_cast<const uint4*>(v.ximg + i);
+  } else {
+    const E* full = static_cast<const E*>(v.full);
+    for (uint32_t i = threadIdx.x; i < hot_n; i += NT) hot[i] = full[i];
+  }
   __syncthreads();
   const __attribute__((address_space(1))) E* gfull = (const __attribute__((address_space(1))) E*)v.full;
   const uint32_t K = v.nclasses, cn = cls['\n'];
-  FullDfa<E> d{hot, gfull, cls, K, hot_n};
+  FullDfa<E, XR> d{hot, gfull, cls, K, hot_n};
   if constexpr (XR) {
-    d.xr = xr;
+    d.xr = reinterpret_cast<const uint2*>(lbuf + v.xr_off);
     d.xh = v.x_hot;
-    d.xn = v.x_rec;
   }
   auto next = [&](uint32_t s, uint32_t c) -> uint32_t { return d.next_cls(s, c); };
   // state after [a, e) from s, stopping at the absorbing MATCHED state
@@ -2676,25 +2702,25 @@ constexpr int kLongDfaThreads = 1024;
 constexpr uint32_t kLongDfaHotBytes = 120 * 1024;  // rows alone (u32 DFAs)
 constexpr uint32_t kLongDfaLdsBytes = 158 * 1024;  // rows + DfaXRec (u16 DFAs)
 
-template <typename E>
+template <typename E, bool XI>
 __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg_kernel(LongDfaArgs la) {
   __shared__ uint32_t cls[256];
   __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLongDfaLdsBytes];
   if (threadIdx.x < 256) cls[threadIdx.x] = la.cls[threadIdx.x];
   E* const hot = reinterpret_cast<E*>(lbuf);
-  const E* full = static_cast<const E*>(la.full);
-  const bool xd = sizeof(E) == 2 && la.xrec != nullptr;
-  const uint32_t hot_n = xd ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
-  for (uint32_t i = threadIdx.x; i < hot_n; i += kLongDfaThreads) hot[i] = full[i];
-  uint2* const xr = reinterpret_cast<uint2*>(lbuf + ((hot_n * sizeof(E) + 7u) & ~7u));
-  const uint32_t xn = xd ? la.x_rec : 0u;
-  for (uint32_t i = threadIdx.x; i < xn; i += kLongDfaThreads) xr[i] = la.xrec[i];
+  const uint32_t hot_n = XI ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
+  if constexpr (XI) {
+    for (uint32_t i = threadIdx.x * 16u; i < la.ximg_bytes; i += kLongDfaThreads * 16u)
+      *reinterpret_cast<uint4*>(lbuf + i) = *reinterpret_cast<const uint4*>(la.ximg + i);
+  } else {
+    const E* full = static_cast<const E*>(la.full);
+    for (uint32_t i = threadIdx.x; i < hot_n; i += kLongDfaThreads) hot[i] = full[i];
+  }
   __syncthreads();
-  FullDfa<E> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, hot_n};
-  if (xd) {
-    d.xr = xr;
+  FullDfa<E, XI> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, hot_n};
+  if constexpr (XI) {
+    d.xr = reinterpret_cast<const uint2*>(lbuf + la.xr_off);
     d.xh = la.x_hot;
-    d.xn = xn;
   }
   // two segments per lane (g and g + half), stepped byte by byte in lockstep:
   // the chain is a dependent table read per byte, so two chains per lane
@@ -2730,7 +2756,8 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg_kernel(LongDfaAr
         if (p == beg_a) ga = sa;
         if (p == beg_b) gb = sb;
         const uint32_t xa = (wa[j >> 2] >> (8 * (j & 3))) & 0xffu, xb = (wb[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        const uint32_t na = d.next(sa, xa), nb = d.next(sb, xb);
+        uint32_t na = sa, nb = sb;
+        d.next2(na, xa, nb, xb);
         sa = (p >= lo_a && p < end_a) ? na : sa;
         sb = (p >= lo_b && p < end_b) ? nb : sb;
       }
@@ -3147,9 +3174,11 @@ hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
     uint64_t grid = ((la.nseg + 1) / 2 + kLongDfaThreads - 1) / kLongDfaThreads;
     if (grid > 65536) grid = 65536;
     if (u32)
-      hipLaunchKernelGGL(long_dfa_seg_kernel<uint32_t>, dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
+      hipLaunchKernelGGL((long_dfa_seg_kernel<uint32_t, false>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
+    else if (la.ximg)
+      hipLaunchKernelGGL((long_dfa_seg_kernel<uint16_t, true>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
     else
-      hipLaunchKernelGGL(long_dfa_seg_kernel<uint16_t>, dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
+      hipLaunchKernelGGL((long_dfa_seg_kernel<uint16_t, false>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
   }
   uint64_t grid = (la.npend + 255) / 256;
   if (grid > 4096) grid = 4096;
@@ -3174,7 +3203,7 @@ hipError_t verify_candidates(const VerifyArgs& v, bool candidates, hipStream_t s
     hipLaunchKernelGGL(verify_nfa_kernel<kNfaMaxWords>, dim3(grid), dim3(256), 0, stream, v);
   else if (v.full_u32)
     hipLaunchKernelGGL((verify_kernel<uint32_t, false>), dim3(grid), dim3(256), 0, stream, v);
-  else if (v.xrec)
+  else if (v.ximg)
     // one persistent 1024-thread workgroup per CU: the LDS copy once per CU
     hipLaunchKernelGGL((verify_kernel<uint16_t, true>), dim3(std::min<uint64_t>(v.num_cus, (v.ntiles + 15) / 16)),
                        dim3(1024), 0, stream, v);

@@ -140,8 +140,8 @@ struct dgrep_ctx {
   uint32_t blob_start = 0, blob_start_m = 0;  // start / start_m in d_full's (breadth-first) ids
   uint32_t blob_matched = UINT32_MAX;          // the absorbing accepting state in d_full's ids (none: UINT32_MAX)
   uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
-  uint2* d_xrec = nullptr;                     // long_dfa_seg_kernel's DfaXRec (u16 DFAs; see LongDfaArgs)
-  uint32_t x_hot = 0, x_rec = 0;
+  uint8_t* d_ximg = nullptr;                   // the whole-DFA LDS image (build_ximg; u16 DFAs that fit)
+  uint32_t ximg_bytes = 0, x_hot = 0, x_rec = 0, xr_off = 0;
   uint32_t* d_nfa = nullptr;                   // DGREP_DFA_PARTIAL: the NFA program (verify_nfa_kernel)
   uint32_t nfa_words = 0;                      // its position-set words
   int blocks_per_cu = 1;
@@ -270,53 +270,67 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
   return DGREP_OK;
 }
 
-// long_dfa_seg_kernel's LDS copy of a u16 DFA F ([S][K], breadth-first ids):
-// the first *hot rows whole, then a DfaXRec (scan_common.h) for each of the
-// next states while the LDS budget lasts -- its default = the resident row
-// differing from its own in the fewest classes (exhaustive, stopping at one
-// difference; config 4: 4,978 records, 30 ms), exceptions <= 2, else no
-// default. The rows get what the records leave: all S states covered when
-// 8 S fits beside at least 64 rows, else half the budget each.
+// The LDS image through which long_dfa_seg_kernel and verify_kernel read a
+// whole u16 DFA F ([S][K], breadth-first ids) with no HBM access on the chain:
+// rows [0, H) whole; then one DfaXRec (scan_common.h) for each state in
+// [H, S) -- its default = the resident row differing from its own in the
+// fewest classes (exhaustive, stopping at one difference; config 4: 30 ms),
+// with the <= 2 differing classes as exceptions; a state no resident row
+// comes within two classes of gets its own row after the first H (an EXTRA
+// row, its record's default, no exceptions). Layout: rows (H + X) * K u16,
+// records at *xr_off (8-aligned). H is the most rows that leave room for
+// everything within `budget`; false if even 64 rows do not (the kernels then
+// keep the first rows and read the rest from HBM).
 #ifndef DGREP_LONG_XREC
 #define DGREP_LONG_XREC 1
 #endif
-// verify_kernel on the same LDS copy (one 1024-thread workgroup per CU)
+// verify_kernel on the same LDS image (one 1024-thread workgroup per CU)
 #ifndef DGREP_VERIFY_XREC
 #define DGREP_VERIFY_XREC 1
 #endif
-static void build_xrec(const uint16_t* F, uint32_t S, uint32_t K, uint32_t budget, uint32_t* hot,
-                       std::vector<uint2>* out) {
-  out->clear();
-  const uint64_t row = 2ull * K, B = budget - 8;  // 8: the records' alignment
-  uint64_t H = 0, R = 0;
-  if (B > 8ull * S && (B - 8ull * S) / (row - 8) >= 64) {
-    H = std::min<uint64_t>(S, (B - 8ull * S) / (row - 8));
-    R = S - H;
-  } else {
-    H = std::min<uint64_t>(S, B / 2 / row);
-    R = std::min<uint64_t>(S - H, (B - H * row) / 8);
-  }
-  *hot = uint32_t(H);
-  out->resize(R);
-  for (uint64_t j = 0; j < R; ++j) {
-    const uint16_t* f = F + (H + j) * K;
-    uint32_t best = 3, bd = 0xffffu;
-    for (uint64_t d = 0; d < H && best > 1; ++d) {
-      const uint16_t* g = F + d * K;
-      uint32_t diff = 0;
-      for (uint32_t k = 0; k < K && diff < best; ++k) diff += f[k] != g[k];
-      if (diff < best) { best = diff; bd = uint32_t(d); }
-    }
-    uint2 r = make_uint2(0xffffu | (kXNone << 16) | (kXNone << 24), 0u);
-    if (bd != 0xffffu) {
+static bool build_ximg(const uint16_t* F, uint32_t S, uint32_t K, uint32_t budget, std::vector<uint8_t>* img,
+                       uint32_t* hot, uint32_t* xr_off) {
+  const uint64_t row = 2ull * K;
+  if (K >= kXNone || row <= 8 || budget < 8ull * S + 64 * row + 8) return false;
+  uint64_t H = std::min<uint64_t>(S, (budget - 8 - 8ull * S) / (row - 8));
+  for (int attempt = 0; attempt < 8 && H >= 64; ++attempt) {
+    const uint64_t R = S - H;
+    std::vector<uint2> rec(R);
+    std::vector<uint32_t> extra;
+    for (uint64_t j = 0; j < R; ++j) {
+      const uint16_t* f = F + (H + j) * K;
+      uint32_t best = 3, bd = 0;
+      for (uint64_t d = 0; d < H && best > 1; ++d) {
+        const uint16_t* g = F + d * K;
+        uint32_t diff = 0;
+        for (uint32_t k = 0; k < K && diff < best; ++k) diff += f[k] != g[k];
+        if (diff < best) { best = diff; bd = uint32_t(d); }
+      }
+      if (best > 2) {
+        rec[j] = make_uint2(uint32_t(H + extra.size()) | (kXNone << 16) | (kXNone << 24), 0u);
+        extra.push_back(uint32_t(H + j));
+        continue;
+      }
       uint32_t cl[2] = {kXNone, kXNone}, nx[2] = {0, 0}, e = 0;
       const uint16_t* g = F + uint64_t(bd) * K;
       for (uint32_t k = 0; k < K; ++k)
         if (f[k] != g[k]) { cl[e] = k; nx[e] = f[k]; ++e; }
-      r = make_uint2(bd | (cl[0] << 16) | (cl[1] << 24), nx[0] | (nx[1] << 16));
+      rec[j] = make_uint2(bd | (cl[0] << 16) | (cl[1] << 24), nx[0] | (nx[1] << 16));
     }
-    (*out)[j] = r;
+    const uint64_t off = ((H + extra.size()) * row + 7) & ~7ull, bytes = (off + 8 * R + 15) & ~15ull;
+    if (bytes > budget || H + extra.size() > 0xffffu) {
+      H -= std::min<uint64_t>(H, (bytes - budget) / (row - 8) + 1 + extra.size());
+      continue;
+    }
+    img->assign(bytes, 0);
+    memcpy(img->data(), F, H * row);
+    for (size_t x = 0; x < extra.size(); ++x) memcpy(img->data() + (H + x) * row, F + uint64_t(extra[x]) * K, row);
+    memcpy(img->data() + off, rec.data(), 8 * R);
+    *hot = uint32_t(H);
+    *xr_off = uint32_t(off);
+    return true;
   }
+  return false;
 }
 
 // The pair stepper's LDS image (StepPair, scan_dfa.hip) from the blob's DFA:
@@ -648,7 +662,7 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_xrec, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
+  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_ximg, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
                   c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_seg_from, c->d_seg_state, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_order, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
@@ -774,9 +788,9 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_nfa = nullptr;
   if (c->d_full) HIPCHK(hipFree(c->d_full));
   c->d_full = nullptr;
-  if (c->d_xrec) HIPCHK(hipFree(c->d_xrec));
-  c->d_xrec = nullptr;
-  c->x_hot = c->x_rec = 0;
+  if (c->d_ximg) HIPCHK(hipFree(c->d_ximg));
+  c->d_ximg = nullptr;
+  c->ximg_bytes = c->x_hot = c->x_rec = c->xr_off = 0;
   if (pair_ok || word_ok) {
     // image built above
   } else if (filter_ok && partial) {
@@ -816,14 +830,14 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     HIPCHK(hipMalloc(&c->d_full, full.size()));
     HIPCHK(hipMemcpy(c->d_full, full.data(), full.size(), hipMemcpyHostToDevice));
     c->verify_hot = uint32_t(std::min<size_t>(ne, verify_hot_bytes() / esz)) / K * K;
-    if (!c->full_u32 && K < kXNone) {
-      std::vector<uint2> xr;
-      build_xrec(reinterpret_cast<const uint16_t*>(full.data()), S, K, long_dfa_lds_bytes(), &c->x_hot, &xr);
-      c->x_rec = uint32_t(xr.size());
-      if (!xr.empty()) {
-        HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_xrec), xr.size() * sizeof(uint2)));
-        HIPCHK(hipMemcpy(c->d_xrec, xr.data(), xr.size() * sizeof(uint2), hipMemcpyHostToDevice));
-      }
+    std::vector<uint8_t> ximg;
+    if (!c->full_u32 &&
+        build_ximg(reinterpret_cast<const uint16_t*>(full.data()), S, K, long_dfa_lds_bytes(), &ximg, &c->x_hot,
+                   &c->xr_off)) {
+      c->x_rec = S - c->x_hot;
+      c->ximg_bytes = uint32_t(ximg.size());
+      HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_ximg), ximg.size()));
+      HIPCHK(hipMemcpy(c->d_ximg, ximg.data(), ximg.size(), hipMemcpyHostToDevice));
     }
     if (!c->d_cls) HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_cls), 256));
     HIPCHK(hipMemcpy(c->d_cls, h.byte_class, 256, hipMemcpyHostToDevice));
@@ -1072,9 +1086,10 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   la.seg_off = c->d_seg_off;
   la.pend = c->d_pend;
   la.npend = npend;
-  la.xrec = DGREP_LONG_XREC ? c->d_xrec : nullptr;
+  la.ximg = DGREP_LONG_XREC ? c->d_ximg : nullptr;
+  la.ximg_bytes = c->ximg_bytes;
   la.x_hot = c->x_hot;
-  la.x_rec = c->x_rec;
+  la.xr_off = c->xr_off;
   HIPCHK(long_lines_dfa(la, c->full_u32, c->stream));
   // the host vectors are read by the async copies above: wait before they go
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -1306,9 +1321,10 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     v.nfa_words = c->nfa_words;
     v.matched = c->d_nfa ? UINT32_MAX : c->blob_matched;
     v.pend = c->d_pend;
-    v.xrec = DGREP_VERIFY_XREC ? c->d_xrec : nullptr;
+    v.ximg = DGREP_VERIFY_XREC ? c->d_ximg : nullptr;
+    v.ximg_bytes = c->ximg_bytes;
     v.x_hot = c->x_hot;
-    v.x_rec = c->x_rec;
+    v.xr_off = c->xr_off;
     v.num_cus = uint32_t(c->num_cus);
     HIPCHK(hipEventRecord(c->ev4, c->stream));
     if (npend && park_maps) {

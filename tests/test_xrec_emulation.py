@@ -1,12 +1,13 @@
 """CPU emulation of the default-row records of long_dfa_seg_kernel (DfaXRec in
-csrc/kernels/scan_common.h, built by build_xrec in
+csrc/kernels/scan_common.h, built by build_ximg in
 csrc/runtime/dgrep_runtime.hip, read by FullDfa::next in
 csrc/kernels/scan_dfa.hip).
 
 A u16 DFA's first H breadth-first rows sit in LDS whole; each further state
 gets an 8-byte record: the resident row that differs from its own in the
 fewest classes (its DEFAULT), plus at most two (class, next state)
-exceptions. The emulation restates the construction in numpy and checks that
+exceptions; a state no resident row comes within two classes of gets an extra
+row of its own as default (build_ximg). The emulation restates the construction in numpy and checks that
 the record lookup reproduces every entry of the table, for the configs'
 keyword automaton and a few other filter-sized patterns. The GPU long-line
 tests (tests/test_gpu_long_lines.py) check the C++ builder and the kernel."""
@@ -44,40 +45,40 @@ def bfs_table(cp):
     return bid[T[np.array(order)]]
 
 
-def build_xrec(F, budget=BUDGET):
+def build_ximg(F, budget=BUDGET):
+    """(H, extra rows, records): rows [0, H) resident, records for [H, S);
+    a state no resident row comes within two classes of gets an extra row."""
     S, K = F.shape
-    row, B = 2 * K, budget - 8
-    if B > 8 * S and (B - 8 * S) // (row - 8) >= 64:
-        H = min(S, (B - 8 * S) // (row - 8))
-        R = S - H
-    else:
-        H = min(S, B // 2 // row)
-        R = min(S - H, (B - H * row) // 8)
-    recs = []
-    for j in range(R):
-        f = F[H + j]
-        diff = (F[:H] != f).sum(1)
-        d = int(np.argmin(diff))
-        if diff[d] > 2:
-            recs.append((0xFFFF, NONE, NONE, 0, 0))
-            continue
-        ex = [(int(k), int(f[k])) for k in np.flatnonzero(F[d] != f)] + [(NONE, 0), (NONE, 0)]
-        recs.append((d, ex[0][0], ex[1][0], ex[0][1], ex[1][1]))
-    return H, recs
+    row = 2 * K
+    H = min(S, (budget - 8 - 8 * S) // (row - 8))
+    while H >= 64:
+        recs, extra = [], []
+        for j in range(S - H):
+            f = F[H + j]
+            diff = (F[:H] != f).sum(1)
+            d = int(np.argmin(diff))
+            if diff[d] > 2:
+                recs.append((H + len(extra), NONE, NONE, 0, 0))
+                extra.append(H + j)
+                continue
+            ex = [(int(k), int(f[k])) for k in np.flatnonzero(F[d] != f)] + [(NONE, 0), (NONE, 0)]
+            recs.append((d, ex[0][0], ex[1][0], ex[0][1], ex[1][1]))
+        off = ((H + len(extra)) * row + 7) & ~7
+        size = (off + 8 * len(recs) + 15) & ~15
+        if size <= budget:
+            return H, extra, recs, size
+        H -= (size - budget) // (row - 8) + 1 + len(extra)
+    return None
 
 
-def lookup(F, H, recs, s, c):
+def lookup(F, H, extra, recs, s, c):
     if s < H:
         return int(F[s, c])
-    if s - H < len(recs):
-        d, c1, c2, n1, n2 = recs[s - H]
-        if c == c1:
-            return n1
-        if c == c2:
-            return n2
-        if d != 0xFFFF:
-            return int(F[d, c])
-    return int(F[s, c])  # HBM
+    d, c1, c2, n1, n2 = recs[s - H]
+    t = int(F[d, c]) if d < H else int(F[extra[d - H], c])
+    t = n2 if c == c2 else t
+    t = n1 if c == c1 else t
+    return t
 
 
 def patterns():
@@ -94,11 +95,11 @@ def test_xrec_lookup_reproduces_the_table(pattern):
     S, K = F.shape
     if S <= 256:
         pytest.skip("not a filter-sized DFA")
-    H, recs = build_xrec(F)
-    assert H >= 64
+    H, extra, recs, _ = build_ximg(F)
+    assert H >= 64 and H + len(recs) == S
     for s in range(S):
         for c in range(K):
-            assert lookup(F, H, recs, s, c) == F[s, c], (s, c)
+            assert lookup(F, H, extra, recs, s, c) == F[s, c], (s, c)
 
 
 def test_xrec_covers_config4():
@@ -106,10 +107,8 @@ def test_xrec_covers_config4():
     all but a handful with a default."""
     F = bfs_table(dgrep.CompiledPattern(patterns()[0]))
     S, K = F.shape
-    H, recs = build_xrec(F)
-    assert H + len(recs) == S
-    assert H * 2 * K + 8 * len(recs) <= BUDGET
-    nodef = sum(1 for r in recs if r[0] == 0xFFFF)
-    assert nodef <= 8, nodef
-    ex = collections.Counter((r[1] != NONE) + (r[2] != NONE) for r in recs if r[0] != 0xFFFF)
+    H, extra, recs, size = build_ximg(F)
+    assert H + len(recs) == S and size <= BUDGET
+    assert len(extra) <= 8, len(extra)
+    ex = collections.Counter((r[1] != NONE) + (r[2] != NONE) for r in recs if r[0] < H)
     assert ex[1] > 10 * ex[2]
