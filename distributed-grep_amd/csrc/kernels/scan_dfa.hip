@@ -2773,6 +2773,92 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg_kernel(LongDfaAr
   }
 }
 
+// One segment per lane, read in 64-byte blocks (four 16-B loads, the next
+// block in flight while this one is stepped). Two segments per lane in
+// 16-B pieces kept 2,048 read streams per CU live, more 128-B lines than L2
+// holds: each line came from HBM several times (long_c4 seg kernel 21 ms per
+// 16 GiB, 0.67 TB/s of segment bytes).
+#ifndef DGREP_SEG_ONE
+#define DGREP_SEG_ONE 1
+#endif
+// 16-B pieces per block (4: 64 B, half a line: eight pieces spill at 1024 threads)
+#ifndef DGREP_SEG_PIECES
+#define DGREP_SEG_PIECES 4
+#endif
+constexpr int kSegPieces = DGREP_SEG_PIECES;
+template <typename E, bool XI>
+__global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaArgs la) {
+  __shared__ uint32_t cls[256];
+  __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLongDfaLdsBytes];
+  if (threadIdx.x < 256) cls[threadIdx.x] = la.cls[threadIdx.x];
+  E* const hot = reinterpret_cast<E*>(lbuf);
+  const uint32_t hot_n = XI ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
+  if constexpr (XI) {
+    for (uint32_t i = threadIdx.x * 16u; i < la.ximg_bytes; i += kLongDfaThreads * 16u)
+      *reinterpret_cast<uint4*>(lbuf + i) = *reinterpret_cast<const uint4*>(la.ximg + i);
+  } else {
+    const E* full = static_cast<const E*>(la.full);
+    for (uint32_t i = threadIdx.x; i < hot_n; i += kLongDfaThreads) hot[i] = full[i];
+  }
+  __syncthreads();
+  FullDfa<E, XI> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, hot_n};
+  if constexpr (XI) {
+    d.xr = reinterpret_cast<const uint2*>(lbuf + la.xr_off);
+    d.xh = la.x_hot;
+  }
+  // one DFA step, the cold path behind a ballot
+  auto step = [&](uint32_t s, uint32_t byte) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t c = cls[byte];
+    const uint32_t i = __umul24(s, d.K) + c;
+    uint32_t t = uint32_t(hot[min(i, hot_n - 1u)]);
+    const bool k = i >= hot_n;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(k) != 0, 0)) {
+      if (k) t = d.cold(s, c, i);
+    }
+    return t;
+  };
+  // state after bytes [a, e) from s: the bytes up to the first 64-B boundary
+  // and after the last one singly, the blocks between unrolled with no
+  // position test, the next block in flight
+  auto run = [&](uint64_t a, uint64_t e, uint32_t s) __attribute__((always_inline)) -> uint32_t {
+    constexpr uint64_t kB = 16u * kSegPieces;
+    const uint64_t A = min(e, (a + kB - 1) & ~(kB - 1)), Eb = max(A, e & ~(kB - 1));
+    for (uint64_t p = a; p < A; ++p) s = step(s, la.data[p]);
+    if (A < Eb) {
+      const uint4* src = reinterpret_cast<const uint4*>(la.data + A);
+      const uint64_t nb = (Eb - A) / kB;
+      uint4 cur[kSegPieces], nxt[kSegPieces];
+#pragma unroll
+      for (int k = 0; k < kSegPieces; ++k) cur[k] = src[k];
+      for (uint64_t blk = 0; blk < nb; ++blk) {
+        const uint64_t nx = blk + 1 < nb ? blk + 1 : blk;  // the last block re-reads itself
+#pragma unroll
+        for (int k = 0; k < kSegPieces; ++k) nxt[k] = src[nx * kSegPieces + k];
+#pragma unroll
+        for (int j = 0; j < 16 * kSegPieces; ++j) {
+          const uint4 v = cur[j >> 4];
+          const uint32_t w = (j & 15) < 4 ? v.x : (j & 15) < 8 ? v.y : (j & 15) < 12 ? v.z : v.w;
+          s = step(s, (w >> (8 * (j & 3))) & 0xffu);
+        }
+#pragma unroll
+        for (int k = 0; k < kSegPieces; ++k) cur[k] = nxt[k];
+      }
+    }
+    for (uint64_t p = Eb; p < e; ++p) s = step(s, la.data[p]);
+    return s;
+  };
+  for (uint64_t g = uint64_t(blockIdx.x) * kLongDfaThreads + threadIdx.x; g < la.nseg;
+       g += uint64_t(gridDim.x) * kLongDfaThreads) {
+    const LongSeg A = la.seg[g];
+    const uint64_t fa = la.seg_from[g];
+    // the guess: the state after the lookback [fa, begin) from start (none
+    // for a line's first segment)
+    const uint32_t guess = A.begin == fa ? la.start : run(fa, A.begin, la.start);
+    la.seg_guess[g] = guess;
+    la.seg_exit[g] = run(A.begin, A.end, guess);
+  }
+}
+
 template <typename E>
 __global__ __launch_bounds__(256) void long_dfa_fix_kernel(LongDfaArgs la) {
   __shared__ uint32_t cls[256];
@@ -3166,11 +3252,21 @@ hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream) {
 }
 
 uint32_t long_lookback() { return kLongLookback; }
+uint32_t long_segs_per_lane() { return DGREP_SEG_ONE ? 1u : 2u; }
 uint32_t long_dfa_hot_bytes() { return kLongDfaHotBytes; }
 uint32_t long_dfa_lds_bytes() { return kLongDfaLdsBytes; }
 
 hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
-  if (la.nseg) {
+  if (la.nseg && DGREP_SEG_ONE) {
+    uint64_t grid = (la.nseg + kLongDfaThreads - 1) / kLongDfaThreads;
+    if (grid > 65536) grid = 65536;
+    if (u32)
+      hipLaunchKernelGGL((long_dfa_seg1_kernel<uint32_t, false>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
+    else if (la.ximg)
+      hipLaunchKernelGGL((long_dfa_seg1_kernel<uint16_t, true>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
+    else
+      hipLaunchKernelGGL((long_dfa_seg1_kernel<uint16_t, false>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
+  } else if (la.nseg) {
     uint64_t grid = ((la.nseg + 1) / 2 + kLongDfaThreads - 1) / kLongDfaThreads;
     if (grid > 65536) grid = 65536;
     if (u32)

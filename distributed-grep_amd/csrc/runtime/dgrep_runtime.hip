@@ -92,6 +92,7 @@ hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream);
 uint32_t long_lookback();
 uint32_t long_dfa_hot_bytes();
 uint32_t long_dfa_lds_bytes();
+uint32_t long_segs_per_lane();
 uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
@@ -1041,8 +1042,8 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   // workgroup per CU): a second, partly filled round held half the CUs idle
   // for a whole segment (long_c4: 384 workgroups over 256 CUs). Each line adds
   // at most one partial segment, hence the npend in the divisor. >= 16 KiB.
-  const uint64_t lanes2 = uint64_t(c->num_cus) * 2048;
-  const uint64_t div = npend < lanes2 / 2 ? lanes2 - npend : uint64_t(c->num_cus) * 3072;
+  const uint64_t lanes2 = uint64_t(c->num_cus) * 1024 * long_segs_per_lane();
+  const uint64_t div = npend < lanes2 / 2 ? lanes2 - npend : uint64_t(c->num_cus) * 1536 * long_segs_per_lane();
   const uint64_t seg = std::max<uint64_t>(uint64_t(16) << 10, (total / div + 16) & ~uint64_t(15));
   std::vector<LongSeg> segs;
   std::vector<uint64_t> from, off(npend + 1, 0);
