@@ -2790,7 +2790,8 @@ template <typename E, bool XI>
 __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaArgs la) {
   __shared__ uint32_t cls[256];
   __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLongDfaLdsBytes];
-  if (threadIdx.x < 256) cls[threadIdx.x] = la.cls[threadIdx.x];
+  // classes pre-scaled to the entry size: a step's table address is one v_mad
+  if (threadIdx.x < 256) cls[threadIdx.x] = uint32_t(la.cls[threadIdx.x]) * uint32_t(sizeof(E));
   E* const hot = reinterpret_cast<E*>(lbuf);
   const uint32_t hot_n = XI ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
   if constexpr (XI) {
@@ -2806,16 +2807,27 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
     d.xr = reinterpret_cast<const uint2*>(lbuf + la.xr_off);
     d.xh = la.x_hot;
   }
-  // one DFA step, the cold path behind a ballot
-  auto step = [&](uint32_t s, uint32_t byte) __attribute__((always_inline)) -> uint32_t {
-    const uint32_t c = cls[byte];
-    const uint32_t i = __umul24(s, d.K) + c;
-    uint32_t t = uint32_t(hot[min(i, hot_n - 1u)]);
-    const bool k = i >= hot_n;
+  // one DFA step on scaled class ce: the entry's LDS address in one v_mad, read
+  // unconditionally (past the resident rows it reads the extra rows, the
+  // records or nothing: LDS is bounds-checked), the cold path behind a ballot
+  const uint32_t KE = la.nclasses * uint32_t(sizeof(E)), hot_end = hot_n * uint32_t(sizeof(E));
+  auto step_c = [&](uint32_t s, uint32_t ce) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t ad = __umul24(s, KE) + ce;
+    uint32_t t = uint32_t(*reinterpret_cast<const E*>(lbuf + ad));
+    const bool k = ad >= hot_end;
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(k) != 0, 0)) {
-      if (k) t = d.cold(s, c, i);
+      if (k) t = d.cold(s, ce / uint32_t(sizeof(E)), ad / uint32_t(sizeof(E)));
     }
     return t;
+  };
+  auto step = [&](uint32_t s, uint32_t byte) __attribute__((always_inline)) -> uint32_t {
+    return step_c(s, cls[byte]);
+  };
+  auto word_cls = [&](uint32_t w, uint32_t (&c)[4]) __attribute__((always_inline)) {
+    c[0] = cls[w & 0xffu];
+    c[1] = cls[(w >> 8) & 0xffu];
+    c[2] = cls[(w >> 16) & 0xffu];
+    c[3] = cls[w >> 24];
   };
   // state after bytes [a, e) from s: the bytes up to the first 64-B boundary
   // and after the last one singly, the blocks between unrolled with no
@@ -2830,15 +2842,23 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
       uint4 cur[kSegPieces], nxt[kSegPieces];
 #pragma unroll
       for (int k = 0; k < kSegPieces; ++k) cur[k] = src[k];
+      // the classes of the next word are read while this word is stepped
+      uint32_t cn[4];
+      word_cls(cur[0].x, cn);
       for (uint64_t blk = 0; blk < nb; ++blk) {
         const uint64_t nx = blk + 1 < nb ? blk + 1 : blk;  // the last block re-reads itself
 #pragma unroll
         for (int k = 0; k < kSegPieces; ++k) nxt[k] = src[nx * kSegPieces + k];
 #pragma unroll
-        for (int j = 0; j < 16 * kSegPieces; ++j) {
-          const uint4 v = cur[j >> 4];
-          const uint32_t w = (j & 15) < 4 ? v.x : (j & 15) < 8 ? v.y : (j & 15) < 12 ? v.z : v.w;
-          s = step(s, (w >> (8 * (j & 3))) & 0xffu);
+        for (int wi = 0; wi < 4 * kSegPieces; ++wi) {
+          const uint32_t c[4] = {cn[0], cn[1], cn[2], cn[3]};
+          const int wn = wi + 1;
+          const uint4 v = wn < 4 * kSegPieces ? cur[wn >> 2] : nxt[0];
+          word_cls((wn & 3) == 0 ? v.x : (wn & 3) == 1 ? v.y : (wn & 3) == 2 ? v.z : v.w, cn);
+          s = step_c(s, c[0]);
+          s = step_c(s, c[1]);
+          s = step_c(s, c[2]);
+          s = step_c(s, c[3]);
         }
 #pragma unroll
         for (int k = 0; k < kSegPieces; ++k) cur[k] = nxt[k];
