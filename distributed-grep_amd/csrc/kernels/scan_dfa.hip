@@ -1416,7 +1416,19 @@ static_assert(kParkAfter % Tune<StepSheng8>::B == 0, "park point must be a block
 // The lane's last line is still open at 2 C (it started in the lane's chunk and
 // crossed the whole next one): park it as PENDING -- state and position go to
 // the pending list, the lane's record for it is resolved by the long-line
-// kernels -- instead of reading on alone.
+// kernels -- instead of reading on alone. The filter parks kParkAfter past C:
+// its parked lines are re-run from their start on the whole DFA anyway, and a
+// lane reading on to 2 C held its wave (63 lanes done at C) for a whole second
+// chunk in every tile holding a long line's start (long_c4 scan 7.3 ms per
+// 16 GiB against C4's 4.3).
+#ifndef DGREP_FILTER_PARK_AFTER
+#define DGREP_FILTER_PARK_AFTER 4096
+#endif
+template <class Step>
+__device__ __forceinline__ uint64_t park_point(uint64_t C) {
+  if constexpr (Step::kKind == kStepFilter && DGREP_FILTER_PARK_AFTER != 0) return C + DGREP_FILTER_PARK_AFTER;
+  return 2 * C;
+}
 template <class Step, int E>
 __device__ __forceinline__ void park_pending(const ScanArgs& a, uint64_t cs, uint64_t pos, LaneRun& r,
                                              const Emitter<E, false>& emit, uint32_t s) {
@@ -1541,7 +1553,7 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
       park_pending<Step, E>(a, cs, uint64_t(C), r, emit, emit.mapsl->x);                   \
       break;                                                                               \
     }                                                                                      \
-    if (park && !maps && pos == 2 * uint64_t(C)) {                                         \
+    if (park && !maps && pos == park_point<Step>(uint64_t(C))) {                           \
       park_pending<Step, E>(a, cs, pos, r, emit, r.s);                                     \
       break;                                                                               \
     }                                                                                      \
@@ -2051,7 +2063,7 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
     const uint32_t len = live ? min(sc, C - lane * sc) : 0u;
     // where the main scan parked the lane's last line (park_pending): C +
     // kParkAfter with Sheng chunk maps, else 2 C -- relative to this sub-lane
-    const uint64_t park = uint64_t(C) + (Step::kKind == kStepSheng8 && a.chunk_map ? kParkAfter : uint64_t(C));
+    const uint64_t park = Step::kKind == kStepSheng8 && a.chunk_map ? uint64_t(C) + kParkAfter : park_point<Step>(uint64_t(C));
     const uint64_t park_at = ol.pend ? park - uint64_t(lane) * sc : 0;
     LaneRun r;
     uint32_t nl = 0, nev = 0;

@@ -525,9 +525,15 @@ def test_filter_long_candidates_wave_verified(filter_ctx):
         lines.append(bytes(body))
         lines.append(b"short line %d" % i)
     data = b"\n".join(lines) + b"\n"
-    # only lines of 16.5-30 KiB: at 32 KiB chunks none is parked (a lane parks
-    # at 2 C), so every dropped candidate went through the wave verifier
-    mid = b"\n".join(l for l in lines if 16500 <= len(l) < 30000) + b"\n"
+    # only lines of 16.5-30 KiB, each right after a '\n' at a 32 KiB chunk's
+    # first byte (filler lines between): at 32 KiB chunks none is parked (the
+    # filter parks a line still open 4 KiB past its owner's chunk end), so
+    # every dropped candidate went through the wave verifier
+    mid = bytearray()
+    for l in lines:
+        if 16500 <= len(l) < 30000:
+            mid += b"z" * ((-len(mid)) % 32768) + b"\n" + l + b"\n"
+    mid = bytes(mid)
     patterns = [b"error", b"(WARN|ERROR) [a-z_]+", b"^ab.*x", b"k[^z]*y",
                 b"(?i)(" + b"|".join(kws) + b")"]
     try:
