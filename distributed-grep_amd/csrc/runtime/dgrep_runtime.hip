@@ -549,6 +549,9 @@ bool build_word_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   return true;
 }
 
+#ifndef DGREP_FILTER_PITCH
+#define DGREP_FILTER_PITCH 1
+#endif
 // The filter stepper's LDS image (StepFilter, scan_dfa.hip): byte classes (kFilterClassBytes),
 // then u16 rows of the DFA's first
 // R - 2 states in breadth-first order from start (start_m at depth 0), as many
@@ -562,9 +565,14 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
                         uint32_t* start, uint32_t* start_m, uint32_t* cand_end, uint32_t excluded = UINT32_MAX) {
   const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
   const uint32_t cn = h.byte_class[uint8_t('\n')];
+  // row pitch P >= K entries with P / 2 odd (DGREP_FILTER_PITCH): consecutive
+  // rows start an odd number of dwords apart, so the rows a wave's lanes sit in
+  // cover the 32 banks in turn (a CPU model of config 4's chain reads: 5.8 ->
+  // 5.6 LDS cycles per read)
+  const uint32_t P = DGREP_FILTER_PITCH ? ((K + 1) & ~1u) + (((K + 1) & 2u) ? 0u : 2u) : K;
   // rows that fit (row_cap: dgrep_set_stepper's test knob)
-  const uint32_t R = std::min<uint32_t>((kFilterImageBytes - kFilterClassBytes) / (2 * K), row_cap);
-  if (R < 4 || uint64_t(R) * K > 65535) return false;
+  const uint32_t R = std::min<uint32_t>((kFilterImageBytes - kFilterClassBytes) / (2 * P), row_cap);
+  if (R < 4 || uint64_t(R) * P > 65535) return false;
   std::vector<uint32_t> order;
   std::vector<uint8_t> seen(S, 0);
   auto visit = [&](uint32_t x) {
@@ -586,23 +594,23 @@ bool build_filter_image(const dgrep_blob_header& h, const uint32_t* trans, uint3
   id[M] = next++;
   const uint32_t CEND = exact ? UINT32_MAX : next++;
   const uint32_t Sf = next;
-  auto to = [&](uint32_t x) { return uint16_t((id[x] == UINT32_MAX ? CAND : id[x]) * K); };
-  img->assign((kFilterClassBytes + size_t(Sf) * K * 2 + 15) & ~size_t(15), 0);
+  auto to = [&](uint32_t x) { return uint16_t((id[x] == UINT32_MAX ? CAND : id[x]) * P); };
+  img->assign((kFilterClassBytes + size_t(Sf) * P * 2 + 15) & ~size_t(15), 0);
   for (int b = 0; b < 256; ++b) img->data()[b] = h.byte_class[b];
   uint16_t* rows = reinterpret_cast<uint16_t*>(img->data() + kFilterClassBytes);
   for (uint32_t i = 0; i < keep; ++i) {
     const uint32_t x = order[i];
-    for (uint32_t k = 0; k < K; ++k) rows[size_t(id[x]) * K + k] = to(trans[size_t(x) * K + k]);
+    for (uint32_t k = 0; k < K; ++k) rows[size_t(id[x]) * P + k] = to(trans[size_t(x) * K + k]);
   }
   if (!exact) {
     for (uint32_t k = 0; k < K; ++k) {
-      rows[size_t(CAND) * K + k] = uint16_t((k == cn ? CEND : CAND) * K);
-      rows[size_t(CEND) * K + k] = to(trans[size_t(h.start) * K + k]);
+      rows[size_t(CAND) * P + k] = uint16_t((k == cn ? CEND : CAND) * P);
+      rows[size_t(CEND) * P + k] = to(trans[size_t(h.start) * K + k]);
     }
   }
-  *start = id[h.start] * K;
-  *start_m = id[M] * K;
-  *cand_end = exact ? UINT32_MAX : CEND * K;
+  *start = id[h.start] * P;
+  *start_m = id[M] * P;
+  *cand_end = exact ? UINT32_MAX : CEND * P;
   return true;
 }
 
