@@ -255,3 +255,29 @@ def test_filter_long_lines_synth_kind4(gpu_ctx):
     assert data.count(b"\n") < 10000  # mostly long lines
     st = _check(gpu_ctx, _c4_pattern(), data)
     assert st["stepper"] == "filter", st
+
+
+def test_filter_long_lines_large_keyword_dfa(gpu_ctx):
+    """3,000 (?i) keywords (18,584 DFA states): the whole-DFA LDS image of the
+    long-line and verification kernels holds ~230 whole rows and a default-row
+    record for every other state (csrc/runtime build_ximg), so most cold steps
+    go through records; long lines with planted keywords and log lines between,
+    bit-exact vs the oracle."""
+    import dgrep
+
+    kws = [k for s in (4, 5, 6) for k in dgrep.synth_keywords(s, 1000)]
+    rnd = random.Random(4242)
+    words = [b"request", b"user", b"cache", b"latency", b"retry", b"shard", b"value", b"node"]
+    parts = []
+    for i in range(8):
+        L = rnd.randrange(256 << 10, 2 << 20)
+        body = bytearray(b" ".join(rnd.choice(words) for _ in range(L // 5))[:L])
+        for _ in range(i % 3):
+            kw = rnd.choice(kws)
+            q = rnd.randrange(L - len(kw))
+            body[q:q + len(kw)] = kw
+        parts.append(bytes(body))
+        parts.append(dgrep.synth_corpus_host(rnd.randrange(100, 20000), 500 + i, 1).rstrip(b"\n"))
+    data = b"\n".join(parts)
+    st = _check(gpu_ctx, b"(?i)(" + b"|".join(kws) + b")", data)
+    assert st["stepper"] == "filter" and st["pending"] > 0, st
