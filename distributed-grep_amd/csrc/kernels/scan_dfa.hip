@@ -1413,22 +1413,23 @@ __device__ __forceinline__ bool lane_done(uint64_t pos, uint64_t C, const LaneRu
 constexpr uint64_t kParkAfter = 4096;
 static_assert(kParkAfter % Tune<StepSheng8>::B == 0, "park point must be a block boundary");
 
-// The lane's last line is still open at 2 C (it started in the lane's chunk and
-// crossed the whole next one): park it as PENDING -- state and position go to
+// The lane's last line is still open kParkLate bytes past its chunk end (it
+// started in the lane's chunk): park it as PENDING -- state and position go to
 // the pending list, the lane's record for it is resolved by the long-line
-// kernels -- instead of reading on alone. The filter parks kParkAfter past C:
-// its parked lines are re-run from their start on the whole DFA anyway, and a
-// lane reading on to 2 C held its wave (63 lanes done at C) for a whole second
-// chunk in every tile holding a long line's start (long_c4 scan 7.3 ms per
-// 16 GiB against C4's 4.3).
-#ifndef DGREP_FILTER_PARK_AFTER
-#define DGREP_FILTER_PARK_AFTER 4096
+// kernels -- instead of reading on alone. Round 5: 4 KiB past C (was 2 C): the
+// resolution goes on from the parked state (the filter's re-runs the line from
+// its start), and a lane reading on to 2 C held its wave (63 lanes done at C)
+// for a whole second chunk in every tile holding a long line's start (long_c4
+// scan 7.3 ms per 16 GiB against C4's 4.3). DGREP_PARK_AFTER=0: 2 C.
+#ifndef DGREP_PARK_AFTER
+#define DGREP_PARK_AFTER 4096
 #endif
 template <class Step>
 __device__ __forceinline__ uint64_t park_point(uint64_t C) {
-  if constexpr (Step::kKind == kStepFilter && DGREP_FILTER_PARK_AFTER != 0) return C + DGREP_FILTER_PARK_AFTER;
+  if constexpr (DGREP_PARK_AFTER != 0) return C + DGREP_PARK_AFTER;
   return 2 * C;
 }
+static_assert(DGREP_PARK_AFTER % 128 == 0, "park point must be a block boundary");
 template <class Step, int E>
 __device__ __forceinline__ void park_pending(const ScanArgs& a, uint64_t cs, uint64_t pos, LaneRun& r,
                                              const Emitter<E, false>& emit, uint32_t s) {
@@ -2063,7 +2064,7 @@ __global__ __launch_bounds__(kOverflowThreads) void scan_overflow_kernel(ScanArg
     const uint64_t cs = ol.cs + uint64_t(lane) * sc;
     const uint32_t len = live ? min(sc, C - lane * sc) : 0u;
     // where the main scan parked the lane's last line (park_pending): C +
-    // kParkAfter with Sheng chunk maps, else 2 C -- relative to this sub-lane
+    // kParkAfter with Sheng chunk maps, else park_point -- relative to this sub-lane
     const uint64_t park = Step::kKind == kStepSheng8 && a.chunk_map ? uint64_t(C) + kParkAfter : park_point<Step>(uint64_t(C));
     const uint64_t park_at = ol.pend ? park - uint64_t(lane) * sc : 0;
     LaneRun r;
