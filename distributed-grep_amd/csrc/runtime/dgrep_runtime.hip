@@ -282,6 +282,9 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 // records at *xr_off (8-aligned). H is the most rows that leave room for
 // everything within `budget`; false if even 64 rows do not (the kernels then
 // keep the first rows and read the rest from HBM).
+#ifndef DGREP_SYNC_SPIN
+#define DGREP_SYNC_SPIN 1
+#endif
 #ifndef DGREP_LONG_XREC
 #define DGREP_LONG_XREC 1
 #endif
@@ -1272,7 +1275,18 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
       HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
                          d_line, d_start, d_len, c->stream));
     HIPCHK(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (DGREP_SYNC_SPIN) {
+      // block until the scan kernel is done (its wake-up latency overlaps the
+      // ordering passes), then poll the short tail (ordering, the 32-B count
+      // copy): the blocking wait alone returned tens of µs after the copy
+      HIPCHK(hipEventSynchronize(c->ev1));
+      hipError_t q;
+      while ((q = hipStreamQuery(c->stream)) == hipErrorNotReady) {
+      }
+      HIPCHK(q);
+    } else {
+      HIPCHK(hipStreamSynchronize(c->stream));
+    }
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     S.scan_ms += ms;  // a re-run scan is counted: it is part of this call's device time
