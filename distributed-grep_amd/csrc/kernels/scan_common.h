@@ -274,19 +274,22 @@ constexpr uint32_t kFilterClassBytes = 256;
 // StepPair's two-byte table T2 (u16 [state][class][class], premultiplied
 // states) must address itself with 16-bit values; its whole LDS image (T2 +
 // T1 + the 2 KiB of u32 byte tables UA, UB) at most kPairMaxImage bytes.
-// (Byte-table swizzles and a u8 class table were measured slower on MI355X:
-// these steppers are VALU-issue-bound)
+// (Byte-table swizzles were measured slower on MI355X: they cost VALU.)
 constexpr uint32_t kPairMaxT2 = 32768;
-// DGREP_PAIR_U8 (off: measured neutral, C3 0.530 vs 0.531 same box, r05): the
-// byte tables are ONE u8 table C[b] = 2 * class(b)
-// at LDS address 0 instead of the u32 UA / UB tables. A u8 table keeps four
-// byte values per dword, so printable ASCII spans 24 dwords in 24 distinct
-// banks and a wave's class reads of text never conflict (u32 entries put 'a',
-// 'A' and '!' in one bank: 47 % of C3's LDS cycles were conflicts, r04); the
-// pair's column offset 2 (c1 K + c2) = C[b0] K + C[b1] costs one v_mad_u32_u24
-// per pair, off the dependent chain.
+// DGREP_PAIR_U8 (on since the end of round 5): the byte tables are ONE u8
+// table C[b] = esz * class(b) at LDS address 0 instead of the u32 UA / UB
+// tables. A u8 table keeps four byte values per dword, so ASCII spans 32
+// dwords in 32 distinct banks and a wave's class reads of text never conflict
+// (u32 entries at 4 b: 4.1 LDS cycles per read on C3's corpus, tools/
+// lds_bank_sim.py; the pair kernel's LDS is ~80 % busy, half of it conflicts);
+// the pair's column offset esz (c1 K + c2) = C[b0] K + C[b1] costs one
+// v_mad_u32_u24 per pair, off the dependent chain (+1.9 VALU per word). The
+// loads are pinned as 32-bit values (an empty asm), or the event branch's i8
+// phis re-mask them. Same-box A/B, C3: 0.585-0.586 -> 0.586-0.593 (round 5's
+// first u8 build, before the pipelined chain and without the pin: neutral).
+// The T2 limit keeps esz (K - 1) < 256 (esz K^2 <= 16 KiB).
 #ifndef DGREP_PAIR_U8
-#define DGREP_PAIR_U8 0
+#define DGREP_PAIR_U8 1
 #endif
 // StepPair's T2 entries are u32 (ds_read_b32) when the whole image fits
 // kPairW32MaxImage, else u16 (DGREP_PAIR_T2_U32=0: always u16). A u16 chain
@@ -295,7 +298,6 @@ constexpr uint32_t kPairMaxT2 = 32768;
 #ifndef DGREP_PAIR_T2_U32
 #define DGREP_PAIR_T2_U32 1
 #endif
-static_assert(!(DGREP_PAIR_U8 && DGREP_PAIR_T2_U32), "u8 byte tables hold 2 class(b): u16 T2 only");
 constexpr uint32_t kPairW32MaxImage = 16384;
 // OR-ed into the stepper kind handed to the scan entry points (scan_dfa,
 // scan_tile_bytes, ...): the pair stepper's u32-entry build

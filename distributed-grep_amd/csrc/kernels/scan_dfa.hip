@@ -293,7 +293,7 @@ struct StepWide {
 // DFA whose two-byte table fits in LDS (2 * S' * K^2 <= kPairMaxT2 bytes; C3's
 // 20-state, 12-class regex: 6 KiB): ONE table lookup per TWO input bytes.
 // LDS image (kPairT2 = 2 KiB of byte tables first, at LDS address 0; with
-// DGREP_PAIR_U8 one u8 table C[b] = 2 class(b) there instead, see scan_common.h):
+// DGREP_PAIR_U8, the default, one u8 table C[b] = esz class(b) there instead, see scan_common.h):
 //   UA, UB (u32 [256] each): UA[b] = 2K*class(b), UB[b] = 2*class(b), so the
 //      pair's column offset 2*(c1*K + c2) = UA[b0] + UB[b1]; the four lookups
 //      of a word share one address (4*b, UB by the instruction's immediate
@@ -331,9 +331,12 @@ struct StepPairT {
   }
   __device__ __forceinline__ Pre prep_bytes(uint32_t x) const {
     if constexpr (DGREP_PAIR_U8) {
-      // C[b] = 2 class(b) (u8 at LDS 0): a0 = 2 (c0 K + c1), a2 = 2 (c2 K + c3)
+      // C[b] = ESZ class(b) (u8 at LDS 0): a0 = ESZ (c0 K + c1), a2 = ESZ (c2 K + c3);
+      // four bytes per dword, so ASCII's class reads never conflict
       const uint8_t* c8 = lds + kBase;
-      const uint32_t c0 = c8[x & 0xffu], c1 = c8[(x >> 8) & 0xffu], c2 = c8[(x >> 16) & 0xffu], c3 = c8[x >> 24];
+      uint32_t c0 = c8[x & 0xffu], c1 = c8[(x >> 8) & 0xffu], c2 = c8[(x >> 16) & 0xffu], c3 = c8[x >> 24];
+      // pinned as 32-bit values (as the filter's class loads)
+      asm("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
       return Pre{__umul24(c0, K) + c1, 0u, __umul24(c2, K) + c3, 0u};
     }
     // byte 0's table offset 4 * b0 as ONE v_lshlrev_b32_sdwa (hipcc emits
@@ -372,7 +375,7 @@ struct StepPairT {
   }
   // single-byte step (rare paths): state id = (premultiplied state - T2 base) / row bytes
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-    const uint32_t c = DGREP_PAIR_U8 ? uint32_t(lds[kBase + b]) >> 1 : ub(b) / ESZ;
+    const uint32_t c = DGREP_PAIR_U8 ? uint32_t(lds[kBase + b]) / ESZ : ub(b) / ESZ;
     return T1[((s - kT2) / div) * K + c];
   }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }

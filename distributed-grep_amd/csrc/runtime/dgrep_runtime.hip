@@ -418,9 +418,9 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
     ub[b] = esz * c;
   }
   if (DGREP_PAIR_U8) {
-    // one u8 table C[b] = 2 class(b) at LDS 0 (over UA); 2 (K - 1) < 256
-    if (2u * (K - 1u) > 255u) return false;
-    for (int b = 0; b < 256; ++b) img->data()[b] = uint8_t(2u * h.byte_class[b]);
+    // one u8 table C[b] = esz class(b) at LDS 0 (over UA); esz (K - 1) < 256
+    if (esz * (K - 1u) > 255u) return false;
+    for (int b = 0; b < 256; ++b) img->data()[b] = uint8_t(esz * h.byte_class[b]);
   }
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
