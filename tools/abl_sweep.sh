@@ -15,6 +15,6 @@ for spec in "$@"; do
   # ABL_PATTERN: scan the workload's split with another pattern (ablation only)
   PAT=(); [ -n "${ABL_PATTERN:-}" ] && PAT=(--pattern "$ABL_PATTERN")
   out=$(DGREP_LIB=$L timeout -k 10 180 python3 $R/bench.py --workload $WL --split-gib $g --base-offset ${o:-0} --alloc-gib ${a:-0} --lane-chunk ${ch:-0} --steps 6 --warmup 2 --no-cpu-baseline --verify none "${PAT[@]}" 2>>"$OUT/err.txt") || { echo "$spec FAILED" >> "$OUT/sweep.txt"; exit 1; }
-  echo "$spec $(echo "$out" | python3 -c 'import json,sys; d=json.load(sys.stdin); r=d["roofline"]; print("value=%.0f ms_step=%.4f kernel=%.0f GB/s frac=%.3f kms=%.4f chunk=%d" % (d["value"], d["ms_per_step"], r["achieved"], r["frac"], r["kernel_ms_avg"], d["config"]["lane_chunk"]))')" >> "$OUT/sweep.txt"
+  echo "$spec $(echo "$out" | python3 -c 'import json,sys; d=json.load(sys.stdin); r=d["roofline"]; print("value=%.0f ms_step=%.4f kernel=%.0f GB/s frac=%.3f kms=%.4f chunk=%d verify_ms=%s" % (d["value"], d["ms_per_step"], r["achieved"], r["frac"], r["kernel_ms_avg"], d["config"]["lane_chunk"], r.get("verify_ms_last")))')" >> "$OUT/sweep.txt"
 done
 echo "abl done"
