@@ -2231,84 +2231,6 @@ __device__ __forceinline__ void verify_tiles(const VerifyArgs& v, Pred&& line_ma
   }
 }
 
-// verify_tiles with two candidates per lane (batches of 128 records):
-// lines_match(a0, e0, a1, e1, k0, k1) decides both at once, so that each lane
-// walks two independent DFA chains. The one-chain walk is bound by LDS latency
-// (one dependent read per byte, 16 waves per CU under the 158 KiB image). An
-// empty range [0, 0) is no line; the records keep their order (half 0, then 1).
-#ifndef DGREP_VERIFY_PAIR
-#define DGREP_VERIFY_PAIR 1
-#endif
-template <class Pred2, class WavePred>
-__device__ __forceinline__ void verify_tiles_pair(const VerifyArgs& v, Pred2&& lines_match, WavePred&& wave_matches) {
-  const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x / 64u;
-  const uint64_t waves = uint64_t(gridDim.x) * wpb;
-  for (uint64_t t = uint64_t(blockIdx.x) * wpb + (threadIdx.x >> 6); t < v.ntiles; t += waves) {
-    const TileInfo ti = v.tiles[t];
-    if (ti.count == 0) continue;
-    uint32_t kept = 0;
-    for (uint32_t k0 = 0; k0 < ti.count; k0 += 128) {
-      StagedLine L[2];
-      bool keep[2], wave[2], cand[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t k = k0 + uint32_t(h) * 64u + lane;
-        const uint64_t src = ti.base + k;
-        keep[h] = wave[h] = cand[h] = false;
-        L[h] = StagedLine{0, 0, 0};
-        if (k < ti.count && src < v.staging_cap) {
-          L[h] = v.staging[src];
-          keep[h] = true;
-          if (L[h].meta & kMetaPend) {
-            const PendingLine P = v.pend[L[h].len_lo];
-            keep[h] = P.matched != 0u;
-            L[h].len_lo = uint32_t(P.len);
-            L[h].meta = staged_rel(L[h]) | (uint32_t(P.len >> 32) << kLenHiShift);
-          } else if (L[h].meta & kMetaCand) {
-            L[h].meta &= ~kMetaCand;
-            if (staged_len(L[h]) > kVerifyWaveBytes)
-              wave[h] = true;
-            else
-              cand[h] = true;
-          }
-        }
-      }
-      {
-        const uint64_t a0 = cand[0] ? L[0].start : 0u, e0 = cand[0] ? a0 + staged_len(L[0]) : 0u;
-        const uint64_t a1 = cand[1] ? L[1].start : 0u, e1 = cand[1] ? a1 + staged_len(L[1]) : 0u;
-        bool r0 = false, r1 = false;
-        lines_match(a0, e0, a1, e1, r0, r1);
-        if (cand[0]) keep[0] = r0;
-        if (cand[1]) keep[1] = r1;
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint64_t len = wave[h] ? staged_len(L[h]) : 0u;
-        for (uint64_t wm = __ballot(wave[h]); wm; wm &= wm - 1) {
-          const int j = __ffsll((unsigned long long)wm) - 1;
-          const uint64_t a = (uint64_t(uint32_t(__shfl(uint32_t(L[h].start >> 32), j, 64))) << 32) |
-                             uint32_t(__shfl(uint32_t(L[h].start), j, 64));
-          const uint64_t n = (uint64_t(uint32_t(__shfl(uint32_t(len >> 32), j, 64))) << 32) |
-                             uint32_t(__shfl(uint32_t(len), j, 64));
-          const bool r = wave_matches(a, a + n);
-          if (int(lane) == j) keep[h] = r;
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint64_t m = __ballot(keep[h]);
-        const uint32_t pos = uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
-        if (keep[h]) v.staging[ti.base + kept + pos] = L[h];  // in place: both halves were read above
-        kept += uint32_t(__popcll(m));
-      }
-    }
-    if (lane == 0 && kept != ti.count) {
-      v.tiles[t].count = kept;
-      atomicAdd(v.removed, (unsigned long long)(ti.count - kept));
-    }
-  }
-}
-
 // XR: the whole-DFA LDS image (runtime build_ximg) in one 1024-thread
 // workgroup's LDS, one resident workgroup per CU; else the first
 // kVerifyHotBytes of rows in each 256-thread workgroup's LDS, the rest in HBM
@@ -2346,37 +2268,9 @@ __global__ __launch_bounds__(XR ? 1024 : 256) void verify_kernel(VerifyArgs v) {
     });
     return s;
   };
-  // two lines [a0, e0) and [a1, e1) from start at once (next2: both chains'
-  // reads issued together), each chain stopping at MATCHED; a lane steps both
-  // every byte and keeps a result only inside its line
-  auto run_pair = [&](uint64_t a0, uint64_t e0, uint64_t a1, uint64_t e1, uint32_t& s0,
-                      uint32_t& s1) __attribute__((always_inline)) {
-    uint64_t q0 = a0 & ~uint64_t(15), q1 = a1 & ~uint64_t(15);
-    bool g0 = a0 < e0, g1 = a1 < e1;
-    uint4 n0 = g0 ? *reinterpret_cast<const uint4*>(v.data + q0) : uint4{0, 0, 0, 0};
-    uint4 n1 = g1 ? *reinterpret_cast<const uint4*>(v.data + q1) : uint4{0, 0, 0, 0};
-    while (g0 || g1) {
-      const uint4 w0 = n0, w1 = n1;
-      if (g0 && q0 + 16 < e0) n0 = *reinterpret_cast<const uint4*>(v.data + q0 + 16);
-      if (g1 && q1 + 16 < e1) n1 = *reinterpret_cast<const uint4*>(v.data + q1 + 16);
-      // the block's bytes [lo, hi) that are on the line (32-bit: 0..16)
-      const uint32_t lo0 = a0 > q0 ? uint32_t(a0 - q0) : 0u, hi0 = g0 ? uint32_t(min(e0 - q0, uint64_t(16))) : 0u;
-      const uint32_t lo1 = a1 > q1 ? uint32_t(a1 - q1) : 0u, hi1 = g1 ? uint32_t(min(e1 - q1, uint64_t(16))) : 0u;
-      const uint32_t x0[4] = {w0.x, w0.y, w0.z, w0.w}, x1[4] = {w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-      for (uint32_t j = 0; j < 16; ++j) {
-        uint32_t t0 = s0, t1 = s1;
-        d.next2(t0, (x0[j >> 2] >> (8 * (j & 3))) & 0xffu, t1, (x1[j >> 2] >> (8 * (j & 3))) & 0xffu);
-        s0 = (j >= lo0 && j < hi0) ? t0 : s0;  // MATCHED is absorbing within a line
-        s1 = (j >= lo1 && j < hi1) ? t1 : s1;
-      }
-      q0 += 16;
-      q1 += 16;
-      g0 = g0 && q0 < e0 && s0 != v.matched;
-      g1 = g1 && q1 < e1 && s1 != v.matched;
-    }
-  };
-  auto wave_pred = [&](uint64_t a, uint64_t e) {
+  verify_tiles(
+      v, [&](uint64_t a, uint64_t e) { return next(run(a, e, v.start), cn) == v.start_m; },
+      [&](uint64_t a, uint64_t e) {
         // a long candidate by the whole wave: lane j runs segment j from a
         // GUESSED entry state (the state after the kVerifyLookback bytes
         // before it, from start: exact for keyword automata such as config
@@ -2396,20 +2290,7 @@ __global__ __launch_bounds__(XR ? 1024 : 256) void verify_kernel(VerifyArgs v) {
             s = run(a + min(n, uint64_t(j) * seg), a + min(n, uint64_t(j + 1) * seg), s);
         }
         return next(s, cn) == v.start_m || s == v.matched;
-      };
-  if constexpr (XR && DGREP_VERIFY_PAIR) {
-    verify_tiles_pair(
-        v,
-        [&](uint64_t a0, uint64_t e0, uint64_t a1, uint64_t e1, bool& r0, bool& r1) {
-          uint32_t s0 = v.start, s1 = v.start;
-          run_pair(a0, e0, a1, e1, s0, s1);
-          r0 = next(s0, cn) == v.start_m;
-          r1 = next(s1, cn) == v.start_m;
-        },
-        wave_pred);
-  } else {
-    verify_tiles(v, [&](uint64_t a, uint64_t e) { return next(run(a, e, v.start), cn) == v.start_m; }, wave_pred);
-  }
+      });
 }
 
 // ---- NFA verification (DGREP_DFA_PARTIAL) -----------------------------------
