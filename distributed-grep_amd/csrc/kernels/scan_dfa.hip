@@ -2966,6 +2966,10 @@ __global__ __launch_bounds__(256) void tile_block_sum_kernel(const TileInfo* til
 }
 
 // one wave per tile: its prefix, then its staged lines copied to their final slots (SoA)
+#ifndef DGREP_ORDER_UNROLL
+#define DGREP_ORDER_UNROLL 4
+#endif
+constexpr uint32_t kOrderUnroll = DGREP_ORDER_UNROLL;
 __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles, const StagedLine* staging,
                                                           uint64_t ntiles, const uint64_t* bsum_c,
                                                           const uint64_t* bsum_l, uint64_t staging_cap,
@@ -2989,13 +2993,27 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
       pl += x.nl;
     }
     const uint64_t o = wave_sum_u64(pc), lb = wave_sum_u64(pl) + 1;
-    for (uint32_t k = lane; k < ti.count; k += 64) {
-      const uint64_t src = ti.base + k, dst = o + k;
-      if (src < staging_cap && dst < capacity) {
-        const StagedLine L = staging[src];
-        line_no[dst] = lb + staged_rel(L);
-        start[dst] = L.start;
-        len[dst] = staged_len(L);
+    // kOrderUnroll records per lane in flight: every load of a round is issued
+    // before its stores (the stores may alias the staging buffer for all the
+    // compiler knows, so a plain loop waited out one HBM latency per 64 records)
+    for (uint32_t k0 = 0; k0 < ti.count; k0 += 64u * kOrderUnroll) {
+      StagedLine L[kOrderUnroll];
+      bool ok[kOrderUnroll];
+#pragma unroll
+      for (uint32_t u = 0; u < kOrderUnroll; ++u) {
+        const uint32_t k = k0 + u * 64u + lane;
+        const uint64_t src = ti.base + k, dst = o + k;
+        ok[u] = k < ti.count && src < staging_cap && dst < capacity;
+        if (ok[u]) L[u] = staging[src];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kOrderUnroll; ++u) {
+        const uint64_t dst = o + k0 + u * 64u + lane;
+        if (ok[u]) {
+          line_no[dst] = lb + staged_rel(L[u]);
+          start[dst] = L[u].start;
+          len[dst] = staged_len(L[u]);
+        }
       }
     }
   }
