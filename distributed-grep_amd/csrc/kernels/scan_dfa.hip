@@ -2970,6 +2970,10 @@ __global__ __launch_bounds__(256) void tile_block_sum_kernel(const TileInfo* til
 #define DGREP_ORDER_UNROLL 4
 #endif
 constexpr uint32_t kOrderUnroll = DGREP_ORDER_UNROLL;
+// streaming (nontemporal) stores for the three output arrays, for A/B
+#ifndef DGREP_ORDER_NT
+#define DGREP_ORDER_NT 0
+#endif
 __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles, const StagedLine* staging,
                                                           uint64_t ntiles, const uint64_t* bsum_c,
                                                           const uint64_t* bsum_l, uint64_t staging_cap,
@@ -3010,9 +3014,15 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
       for (uint32_t u = 0; u < kOrderUnroll; ++u) {
         const uint64_t dst = o + k0 + u * 64u + lane;
         if (ok[u]) {
+#if DGREP_ORDER_NT
+          __builtin_nontemporal_store(lb + staged_rel(L[u]), line_no + dst);
+          __builtin_nontemporal_store(L[u].start, start + dst);
+          __builtin_nontemporal_store(staged_len(L[u]), len + dst);
+#else
           line_no[dst] = lb + staged_rel(L[u]);
           start[dst] = L[u].start;
           len[dst] = staged_len(L[u]);
+#endif
         }
       }
     }
