@@ -31,14 +31,13 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-grep_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 STAGED_LINE_BYTES = 16  # StagedLine written by the scan kernel per match
-FINAL_LINE_BYTES = 24   # the ABI's (u64 line_no, u64 start, u64 len) per match, when the scan places them itself
 
 
-def kernels_timed(stepper, in_scan):
+def kernels_timed(stepper):
     """The kernels dgrep_last_kernel_ms covers for this stepper (roofline.kernel)."""
-    step = {"sheng": "StepSheng8", "pair": "StepPair", "table": "StepTable", "filter": "StepFilter",
-            "wide": "StepWide", "word": "StepWord"}.get(stepper, str(stepper))
-    ks = ["dgrep::scan_dfa8_kernel<dgrep::%s>%s" % (step, " (in-scan ordering)" if in_scan else "")]
+    step = {"sheng": "StepSheng8", "pair": "StepPair", "table": "StepTable", "filter": "StepFilter"}.get(
+        stepper, str(stepper))
+    ks = ["dgrep::scan_dfa8_kernel<dgrep::%s>" % step]
     if stepper == "filter":
         ks.append("dgrep::verify_kernel (candidate lines on the whole DFA)")
     ks.append("dgrep::scan_overflow_kernel / long-line kernels when a scan needs them")
@@ -58,7 +57,7 @@ WORKLOADS = {
                desc="C3: 16 GiB split (seed 3), anchored regex with classes/alternation"),
     "c4": dict(pattern=None, seed=4, kind=1, gib=16.0, verify_window=256 << 10,
                desc="C4: 16 GiB split (seed 4, keywords planted), (?i) alternation of 1,000 seeded keywords, "
-                    "wide DFA (hot rows in LDS, the rest in HBM/L2)"),
+                    "filter stepper (the DFA's shallow states in LDS, candidate lines verified on the whole DFA)"),
     # SURVEY §8d C5 / BASELINE.json configs[4]: 8 splits x 32 GiB, seeds 100-107
     "c5": dict(pattern="error", seed=100, rank_seed_step=1, kind=0, gib=32.0,
                desc="C5: one 32 GiB synthetic log split per GPU (seed 100 + rank), literal 'error'"),
@@ -482,11 +481,9 @@ def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, c
 
     count, kms, stats = m["count"], m["kms"], m["stats"]
     # algorithmic bytes of the timed kernels: the split read once, plus per
-    # matching line the record the kernel leaves -- the ABI's final 24-byte
-    # record when it placed the lines itself (in-scan ordering), else the
-    # 16-byte staged record the ordering passes (not timed) read back
-    in_scan = bool(stats[-1].get("order_in_scan", 0))
-    alg = n + (FINAL_LINE_BYTES if in_scan else STAGED_LINE_BYTES) * count
+    # matching line the 16-byte staged record the ordering passes (not timed)
+    # read back
+    alg = n + STAGED_LINE_BYTES * count
     kern_ms, kern_med = float(np.mean(kms)), float(np.median(kms))
     mine = torch.tensor([m["elapsed"], kern_ms, kern_med, float(alg), float(count)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -551,9 +548,9 @@ def build_line(args, wl, world, rank, dev, n, pattern, seed, m, verified, cpu, c
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": kernels_timed(st["stepper"], in_scan)[0],
-            "kernels_timed": kernels_timed(st["stepper"], in_scan),
-            "record_bytes": FINAL_LINE_BYTES if in_scan else STAGED_LINE_BYTES,
+            "kernel": kernels_timed(st["stepper"])[0],
+            "kernels_timed": kernels_timed(st["stepper"]),
+            "record_bytes": STAGED_LINE_BYTES,
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

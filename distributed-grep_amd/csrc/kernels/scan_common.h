@@ -98,11 +98,7 @@ struct ScanArgs {
   OverflowLane* overflow;
   uint64_t overflow_cap;
   unsigned long long* overflow_count;
-  // kStepWide only: the whole [state][class] u16 table in HBM (L2-resident);
-  // its first `hot_entries` entries are also in the LDS image
-  const uint16_t* wide;
   uint32_t nclasses;
-  uint32_t hot_entries;
   // kStepPair only (byte offsets into the LDS image, see StepPair)
   uint32_t pair_t1;   // single-byte table T1
   uint32_t pair_thr;  // lowest premultiplied shadow state: a pair ending at >= thr holds an event
@@ -110,11 +106,6 @@ struct ScanArgs {
   // kStepFilter only: the premultiplied CAND_END state (a '\n' ends a line that
   // left the LDS-resident part of the DFA: a candidate, verified afterwards)
   uint32_t cand_end;
-  // kStepWord only (byte offsets into the LDS image, see StepWord): the pair
-  // class table PC, the word class table WC (P x P), the word table TW and the
-  // single-byte table T1; bytes per TW row; pair classes; the lowest
-  // premultiplied event state (shadows, start_m) and recheck shadow
-  uint32_t wd_pb, wd_wc, wd_tw, wd_t1, wd_row, wd_thr_e, wd_thr_r;
   // one-chunk-per-lane steppers: per resident thread, spill_per_lane records of
   // HBM the lane moves its full LDS slots to (nullptr: no spilling)
   uint2* spill;
@@ -130,20 +121,8 @@ struct ScanArgs {
   unsigned long long* pend_count;
   // Sheng stepper: the chunk maps instead of chunk_nl (nullptr: none)
   ChunkMap* chunk_map;
-  // tiles claimed after each wave's first (zeroed per launch); with in-scan
-  // ordering, every tile
+  // tiles claimed after each wave's first (zeroed per launch)
   unsigned long long* tile_next;
-  // in-scan ordering (out_line != nullptr; scan_dfa.hip order_tile): the final
-  // SoA output (capacity out_cap) and, per tile, the published aggregate and
-  // inclusive prefixes tagged with this launch's epoch (!= 0)
-  uint64_t* out_line;
-  uint64_t* out_start;
-  uint64_t* out_len;
-  uint64_t out_cap;
-  uint64_t* agg;
-  uint64_t* incl_c;
-  uint64_t* incl_l;
-  uint32_t epoch;
 };
 
 // the long-line kernels' arguments (long_end / long_map / long_fin)
@@ -251,10 +230,10 @@ constexpr int kTileLanes = 64;     // a tile is one wave's 64 chunks
 enum : int {
   kStepTable = 0,   // <= 256 states: u8 [state][byte] table, 260-byte rows
   kStepSheng8 = 1,  // <= 8 states: per-byte 8-state vectors (v_perm stepping)
-  kStepWide = 2,    // <= 65535 states: u16 [state][class] table, hot rows in LDS, all rows in HBM
+  // 2: the r01 wide stepper (u16 rows, cold ones from HBM on the chain), removed in round 6
   kStepPair = 3,    // 2 * states * classes^2 <= kPairMaxT2 bytes: two input bytes per table lookup
   kStepFilter = 4,  // > 256 states: the DFA's shallow part in LDS, lines that leave it verified afterwards
-  kStepWord = 5,    // one table lookup per 4-byte word: the DFA's word functions (few, for most regexes) in LDS
+  // 5: the r05 word stepper (one lookup per 4-byte word), measured slower than pair; removed in round 6
 };
 
 // LDS image of kStepFilter: byte classes [256] (u8), then u16 [state][class]
@@ -271,26 +250,6 @@ constexpr uint32_t kFilterImageBytes = DGREP_FILTER_KIB * 1024;
 // cycles, u32 entries at 4*b 52 %, u64 at 8*b 55 %). C4 kernel 3.18 -> 3.38 TB/s.
 constexpr uint32_t kFilterClassBytes = 256;
 
-// StepPair's two-byte table T2 (u16 [state][class][class], premultiplied
-// states) must address itself with 16-bit values; its whole LDS image (T2 +
-// T1 + the 2 KiB of u32 byte tables UA, UB) at most kPairMaxImage bytes.
-// (Byte-table swizzles were measured slower on MI355X: they cost VALU.)
-constexpr uint32_t kPairMaxT2 = 32768;
-// DGREP_PAIR_U8 (on since the end of round 5): the byte tables are ONE u8
-// table C[b] = esz * class(b) at LDS address 0 instead of the u32 UA / UB
-// tables. A u8 table keeps four byte values per dword, so ASCII spans 32
-// dwords in 32 distinct banks and a wave's class reads of text never conflict
-// (u32 entries at 4 b: 4.1 LDS cycles per read on C3's corpus, tools/
-// lds_bank_sim.py; the pair kernel's LDS is ~80 % busy, half of it conflicts);
-// the pair's column offset esz (c1 K + c2) = C[b0] K + C[b1] costs one
-// v_mad_u32_u24 per pair, off the dependent chain (+1.9 VALU per word). The
-// loads are pinned as 32-bit values (an empty asm), or the event branch's i8
-// phis re-mask them. Same-box A/B, C3: 0.585-0.586 -> 0.586-0.593 (round 5's
-// first u8 build, before the pipelined chain and without the pin: neutral).
-// The T2 limit keeps esz (K - 1) < 256 (esz K^2 <= 16 KiB).
-#ifndef DGREP_PAIR_U8
-#define DGREP_PAIR_U8 1
-#endif
 // StepPair's T2 entries are u32 (ds_read_b32) when the whole image fits
 // kPairW32MaxImage, else u16 (DGREP_PAIR_T2_U32=0: always u16). A u16 chain
 // value carried across the previous word's event branch is re-masked by one
@@ -299,30 +258,15 @@ constexpr uint32_t kPairMaxT2 = 32768;
 #define DGREP_PAIR_T2_U32 1
 #endif
 constexpr uint32_t kPairW32MaxImage = 16384;
+// StepPair's two-byte table T2 ([state][class][class], premultiplied states)
+// addresses itself with 16-bit values: at most kPairMaxT2 bytes, the whole LDS
+// image (class table, T2, T1) at most kPairMaxImage bytes.
+constexpr uint32_t kPairMaxT2 = 32768;
 // OR-ed into the stepper kind handed to the scan entry points (scan_dfa,
 // scan_tile_bytes, ...): the pair stepper's u32-entry build
 constexpr int kKindW32 = 0x100;
 constexpr uint32_t kPairMaxImage = 40960;
 constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the byte tables)
-// StepWord's LDS image (u32 entries, see StepWord): UA, UB [256] at 0 / 1024,
-// PA [K][K] at kWordPA, PB [K][K], WC [P][P], TW [S'][W], T1 [S'][K]; at most
-// kWordMaxImage bytes.
-constexpr uint32_t kWordPA = 2048;
-constexpr uint32_t kWordMaxImage = 16384;
-
-// LDS image of kStepWide: 256 class bytes, then the hottest rows (u16). The
-// runtime renumbers states hottest-first (start, start_m, then BFS order from
-// start), so the shallow states an Aho-Corasick-like automaton spends nearly
-// all its steps in are LDS-resident and the deep ones are read from L2.
-constexpr uint32_t kWideClassBytes = 256;
-#ifndef DGREP_WIDE_HOT_KIB
-#define DGREP_WIDE_HOT_KIB 96
-#endif
-constexpr uint32_t kWideHotBytes = DGREP_WIDE_HOT_KIB * 1024;
-#ifndef DGREP_WIDE_THREADS
-#define DGREP_WIDE_THREADS 1024
-#endif
-constexpr int kWideThreads = DGREP_WIDE_THREADS;  // one workgroup per CU shares one LDS copy
 // The filter's one workgroup per CU: 1024 threads (4 waves per SIMD) with
 // 128-byte load blocks. With 64-byte blocks it fetched 1.82x the split from
 // HBM (each lane's half-read 128-byte lines are evicted before their second

@@ -25,7 +25,7 @@
 //     '\n' counts and run the DFA over it in parallel -- per-piece transition
 //     maps, composed in order -- instead of one lane reading on alone.
 //   * Per 4-byte word: 4 DFA steps by one of the steppers (StepSheng8,
-//     StepPair, StepTable, StepFilter, StepWide: see each struct), newline
+//     StepPair, StepTable, StepFilter: see each struct), newline
 //     bookkeeping by SWAR on the word, and a matching line is detected by
 //     "state == START_M" (rare path).
 //       StepSheng8 (DFA <= 8 states): LDS holds, per input byte b, the 8-byte
@@ -97,15 +97,6 @@
 #ifndef DGREP_TABLE_WAVES
 #define DGREP_TABLE_WAVES 3
 #endif
-#ifndef DGREP_WIDE_CHUNK
-#define DGREP_WIDE_CHUNK 1024
-#endif
-#ifndef DGREP_WIDE_SLOTS
-#define DGREP_WIDE_SLOTS 4
-#endif
-#ifndef DGREP_WIDE_BLOCK
-#define DGREP_WIDE_BLOCK 64
-#endif
 // Pair (C3, 20 states): one chunk per lane, runtime (adaptive) chunk from 4 KiB
 #ifndef DGREP_PAIR_CHUNK
 #define DGREP_PAIR_CHUNK 4096
@@ -118,11 +109,6 @@
 #endif
 #ifndef DGREP_PAIR_WAVES
 #define DGREP_PAIR_WAVES 3
-#endif
-// chunks per lane stepped in lockstep (2: two independent dependency chains
-// per lane, a fixed DGREP_PAIR_CHUNK, 2 waves per SIMD)
-#ifndef DGREP_PAIR_STREAMS
-#define DGREP_PAIR_STREAMS 1
 #endif
 // Filter (C4, > 256 states): one 1024-thread workgroup per CU shares one LDS image
 #ifndef DGREP_FILTER_CHUNK
@@ -248,60 +234,19 @@ struct StepSheng8 {
   }
 };
 
-// DFA of at most 65535 states (large alternations, SURVEY config 4): u16
-// next-state table [state][class]. The hot rows (lowest state numbers, see
-// kWideHotBytes) are read from LDS, the rest from HBM through L2; the branch
-// is per lane and almost always wave-uniform. The class lookups depend only on
-// the input word and are issued a word ahead.
-struct StepWide {
-  static constexpr int kKind = kStepWide;
-  const uint8_t* cls;    // LDS: byte -> class
-  const uint16_t* hot;   // LDS: rows 0 .. hot_entries / nc - 1
-  const uint16_t* full;  // HBM: every row
-  uint32_t nc, hot_entries;
-  __device__ __forceinline__ uint32_t one(uint32_t s, uint32_t c) const {
-    const uint32_t i = __umul24(s, nc) + c;
-    if (__builtin_expect(i < hot_entries, 1)) return hot[i];
-    // global_load_ushort (a generic pointer would compile to flat_load)
-    return ((const __attribute__((address_space(1))) uint16_t*)full)[i];
-  }
-  struct Pre {
-    uint32_t c0, c1, c2, c3;
-  };
-  __device__ __forceinline__ Pre prep(uint32_t x) const {
-    return Pre{cls[x & 0xffu], cls[(x >> 8) & 0xffu], cls[(x >> 16) & 0xffu], cls[x >> 24]};
-  }
-  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
-                                        uint32_t& s3) const {
-    s0 = one(s, p.c0);
-    s1 = one(s0, p.c1);
-    s2 = one(s1, p.c2);
-    s3 = one(s2, p.c3);
-  }
-  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return one(s, p.c0); }
-  __device__ __forceinline__ void rest(const Pre& p, uint32_t f, uint32_t& s0, uint32_t& s1, uint32_t& s2,
-                                       uint32_t& s3) const {
-    s0 = f;
-    s1 = one(s0, p.c1);
-    s2 = one(s1, p.c2);
-    s3 = one(s2, p.c3);
-  }
-  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const { return one(s, cls[b]); }
-  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
-};
-
-// DFA whose two-byte table fits in LDS (2 * S' * K^2 <= kPairMaxT2 bytes; C3's
-// 20-state, 12-class regex: 6 KiB): ONE table lookup per TWO input bytes.
-// LDS image (kPairT2 = 2 KiB of byte tables first, at LDS address 0; with
-// DGREP_PAIR_U8, the default, one u8 table C[b] = esz class(b) there instead, see scan_common.h):
-//   UA, UB (u32 [256] each): UA[b] = 2K*class(b), UB[b] = 2*class(b), so the
-//      pair's column offset 2*(c1*K + c2) = UA[b0] + UB[b1]; the four lookups
-//      of a word share one address (4*b, UB by the instruction's immediate
-//      offset), depend only on the input and are issued a word ahead; u32
-//      entries put byte b in bank b % 32 (text spreads over the banks);
-//   T2 (at kPairT2): u16 [S'][K][K], entry = next state after the pair,
-//      PREMULTIPLIED to its row's LDS address (kPairT2 + id * 2K^2), so the
-//      dependent chain per pair is one v_add3 + one ds_read_u16;
+// DFA whose two-byte table fits in LDS (esz * S' * K^2 <= kPairMaxT2 bytes;
+// C3's 20-state, 12-class regex: 15.6 KiB with u32 entries): ONE table lookup
+// per TWO input bytes. LDS image:
+//   C (u8 [256] at LDS 0): C[b] = esz class(b); four byte values share a
+//      dword, so ASCII's class reads never conflict. The pair's column offset
+//      esz (c1 K + c2) = C[b0] K + C[b1] is one v_mad_u32_u24; the four class
+//      reads of a word depend only on the input and are issued a word ahead.
+//      (u32 byte tables UA[b] + UB[b], rounds 2-4, conflicted on text: 4.1 LDS
+//      cycles per read on C3's corpus, tools/lds_bank_sim.py.)
+//   T2 (at kPairT2): [S'][K][K] entries (u32, or u16 when the image exceeds
+//      16 KiB), entry = next state after the pair, PREMULTIPLIED to its row's
+//      LDS address (kPairT2 + id * row), so the dependent chain per pair is
+//      one v_add3 + one ds_read;
 //   T1: u16 [S'][K] premultiplied single-byte steps (split tail, last-line check).
 // A pair hides the state between its two bytes, so a '\n' FIRST in a pair that
 // ends a matching line (the byte enters start_m) leads to a SHADOW state: a copy
@@ -309,52 +254,30 @@ struct StepWide {
 // states so that shadows, start_m and shadow(start_m) are the highest: a
 // pair-end state >= thr means an event -- at its first byte if it is a shadow
 // other than start_m, at its second byte if it is >= M (start_m or its shadow).
-
 template <uint32_t ESZ>
 struct StepPairT {
   static constexpr int kKind = kStepPair;
   static constexpr uint32_t kEsz = ESZ;  // bytes per T2 entry (u16 / u32)
-  static constexpr uint32_t kBase = 0u;  // UA, UB, then T2 at kPairT2
-  static constexpr uint32_t kT2 = kBase + kPairT2;
+  static constexpr uint32_t kT2 = kPairT2;
   const uint8_t* lds;
   const uint16_t* T1;
   uint32_t thr, M, div, K;
-  // a0 + b1 (a2 + b3) = 2 (c1 * K + c2): premultiplied byte tables
+  // a0 = esz (c0 K + c1), a2 = esz (c2 K + c3): the word's two pair columns
   struct Pre {
-    uint32_t a0, b1, a2, b3;
+    uint32_t a0, a2;
   };
-  __device__ __forceinline__ uint32_t ua(uint32_t b) const {
-    return *reinterpret_cast<const uint32_t*>(lds + kBase + 4u * b);
+  __device__ __forceinline__ Pre prep(uint32_t x) const {
+    uint32_t c0 = lds[x & 0xffu], c1 = lds[(x >> 8) & 0xffu], c2 = lds[(x >> 16) & 0xffu], c3 = lds[x >> 24];
+    // pinned as 32-bit values: carried across a branch as i8 they are re-masked
+    asm("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
+    return Pre{__umul24(c0, K) + c1, __umul24(c2, K) + c3};
   }
-  __device__ __forceinline__ uint32_t ub(uint32_t b) const {
-    return *reinterpret_cast<const uint32_t*>(lds + kBase + 1024u + 4u * b);
-  }
-  __device__ __forceinline__ Pre prep_bytes(uint32_t x) const {
-    if constexpr (DGREP_PAIR_U8) {
-      // C[b] = ESZ class(b) (u8 at LDS 0): a0 = ESZ (c0 K + c1), a2 = ESZ (c2 K + c3);
-      // four bytes per dword, so ASCII's class reads never conflict
-      const uint8_t* c8 = lds + kBase;
-      uint32_t c0 = c8[x & 0xffu], c1 = c8[(x >> 8) & 0xffu], c2 = c8[(x >> 16) & 0xffu], c3 = c8[x >> 24];
-      // pinned as 32-bit values (as the filter's class loads)
-      asm("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
-      return Pre{__umul24(c0, K) + c1, 0u, __umul24(c2, K) + c3, 0u};
-    }
-    // byte 0's table offset 4 * b0 as ONE v_lshlrev_b32_sdwa (hipcc emits
-    // v_lshlrev + v_and for byte 0 while bytes 1-3 get the SDWA form)
-    uint32_t o0;
-    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
-        : "=v"(o0)
-        : "v"(2u), "v"(x));
-    return Pre{*reinterpret_cast<const uint32_t*>(lds + kBase + o0), ub((x >> 8) & 0xffu), ua((x >> 16) & 0xffu),
-               ub(x >> 24)};
-  }
-  __device__ __forceinline__ Pre prep(uint32_t x) const { return prep_bytes(x); }
   __device__ __forceinline__ uint32_t t2(uint32_t off) const {
     if constexpr (ESZ == 4) return *reinterpret_cast<const uint32_t*>(lds + off);
     return *reinterpret_cast<const uint16_t*>(lds + off);
   }
-  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return t2(s + p.a0 + p.b1); }
-  __device__ __forceinline__ uint32_t second(const Pre& p, uint32_t s1) const { return t2(s1 + p.a2 + p.b3); }
+  __device__ __forceinline__ uint32_t first(const Pre& p, uint32_t s) const { return t2(s + p.a0); }
+  __device__ __forceinline__ uint32_t second(const Pre& p, uint32_t s1) const { return t2(s1 + p.a2); }
   __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                         uint32_t& s3) const {
     s1 = first(p, s);
@@ -362,10 +285,7 @@ struct StepPairT {
     s0 = s1;
     s2 = s3;
   }
-  // apply() in two parts: the word's first chain read, then the rest (f comes
-  // from a ds_read_u16; carried across the previous word's event branch it is
-  // re-masked by one v_and: neither __builtin_assume nor a v_mad_u32_u16 in
-  // asm removed it)
+  // apply() in two parts: the word's first chain read (f), then the rest
   __device__ __forceinline__ void rest(const Pre& p, uint32_t f, uint32_t& s0, uint32_t& s1, uint32_t& s2,
                                        uint32_t& s3) const {
     s1 = f;
@@ -375,8 +295,7 @@ struct StepPairT {
   }
   // single-byte step (rare paths): state id = (premultiplied state - T2 base) / row bytes
   __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-    const uint32_t c = DGREP_PAIR_U8 ? uint32_t(lds[kBase + b]) / ESZ : ub(b) / ESZ;
-    return T1[((s - kT2) / div) * K + c];
+    return T1[((s - kT2) / div) * K + uint32_t(lds[b]) / ESZ];
   }
   __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
   __device__ __forceinline__ bool any2(uint32_t s1, uint32_t s3) const { return max(s1, s3) >= thr; }
@@ -391,71 +310,6 @@ struct StepPairT {
 // LLVM keeps the phi as i16), else u16 (twice the states per image)
 using StepPair = StepPairT<4>;
 using StepPair16 = StepPairT<2>;
-
-// DFA with few WORD FUNCTIONS: ONE dependent table lookup per 4-byte word.
-// A word's effect on the DFA is a function S -> S; for the regexes of the
-// configs there are few distinct ones (C3's 20 states x 12 classes: 69 word
-// functions, 27 pair functions), so the runtime (build_word_image) numbers
-// them and the chain per word is s' = TW[s][w] -- one v_lshl_add + one
-// ds_read_u16 (pair stepper: two of each). The word class w depends only on
-// the input, in three table levels: byte classes C[b] (u8), pair classes
-// PC[c0][c1], word classes WC[p01][p23]; run_block_word issues those levels
-// words ahead of the chain, so they never wait on it.
-// Events: a word hides the states between its bytes, so a word whose single
-// '\n' ends a matching line before its last byte leads to an EVENT shadow (a
-// copy of the state its last bytes reach; a '\n' last in the word leaves
-// start_m itself), and a word with two or more '\n' leads to a RECHECK shadow
-// (its events are recomputed byte by byte from the state before it, rare).
-// Ids: the other states, the event shadows, start_m, the recheck shadows --
-// a word ending at >= thr_e holds an event or needs a recheck (>= thr_r).
-struct StepWord {
-  static constexpr int kKind = kStepWord;
-  // LDS image (u32 entries: a value crossing the event branch as a narrower
-  // load would be re-masked by a v_and on every use), at LDS address 0:
-  //   UA, UB [256]: 4 K class(b), 4 class(b)   -> pair index bytes UA[b0] + UB[b1]
-  //   PA, PB [K K] at kWordPA / pb:  4 P pc, 4 pc  -> word index bytes PA[..] + PB[..]
-  //   WC [P P] at wc: 4 w (the word's column bytes in TW)
-  //   TW [S'][W] at tw, rows of `row` bytes: the next state, premultiplied to its row's address
-  //   T1 [S'][K] at t1: single-byte steps, premultiplied
-  const uint8_t* lds;
-  const uint32_t* T1;
-  uint32_t K, pb, wc, thr_e, thr_r, row, tw;
-  __device__ __forceinline__ uint32_t ld(uint32_t a) const { return *reinterpret_cast<const uint32_t*>(lds + a); }
-  __device__ __forceinline__ uint32_t ua(uint32_t b) const { return ld(4u * b); }
-  __device__ __forceinline__ uint32_t ub(uint32_t b) const { return ld(1024u + 4u * b); }
-  __device__ __forceinline__ uint32_t pa(uint32_t ix) const { return ld(kWordPA + ix); }  // ix = UA + UB
-  __device__ __forceinline__ uint32_t pbv(uint32_t ix) const { return ld(pb + ix); }
-  __device__ __forceinline__ uint32_t wcol(uint32_t ix) const { return ld(wc + ix); }    // ix = PA + PB
-  // the stepper's one-word lookups run in run_block_word's pipeline; prep /
-  // apply serve the generic paths (cold starts, single words)
-  struct Pre {
-    uint32_t col;  // the word's column bytes in TW
-  };
-  __device__ __forceinline__ Pre prep(uint32_t x) const {
-    const uint32_t a = pa(ua(x & 0xffu) + ub((x >> 8) & 0xffu));
-    const uint32_t b = pbv(ua((x >> 16) & 0xffu) + ub(x >> 24));
-    return Pre{wcol(a + b)};
-  }
-  __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t col) const { return ld(s + col); }
-  __device__ __forceinline__ void apply(const Pre& p, uint32_t s, uint32_t& s0, uint32_t& s1, uint32_t& s2,
-                                        uint32_t& s3) const {
-    s3 = step(s, p.col);
-    s0 = s1 = s2 = s3;
-  }
-  // single-byte step (rare paths): state id = (premultiplied state - TW base) / row bytes
-  __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-    return T1[((s - tw) / row) * K + (ub(b) >> 2)];
-  }
-  // the exact states after each byte of word x from s (recheck / past-chunk paths)
-  __device__ __forceinline__ void bytes4(uint32_t s, uint32_t x, uint32_t& s0, uint32_t& s1, uint32_t& s2,
-                                         uint32_t& s3) const {
-    s0 = byte(s, x & 0xffu);
-    s1 = byte(s0, (x >> 8) & 0xffu);
-    s2 = byte(s1, (x >> 16) & 0xffu);
-    s3 = byte(s2, x >> 24);
-  }
-  __device__ __forceinline__ static bool is(uint32_t s, uint32_t M) { return s == M; }
-};
 
 // DFA of more than 256 states (large alternations, SURVEY config 4) as a
 // FILTER that lives wholly in LDS: the runtime keeps the DFA's shallowest
@@ -536,20 +390,10 @@ __device__ __forceinline__ StepPair16 make_step<StepPair16>(const uint8_t* lds, 
 }
 
 template <>
-__device__ __forceinline__ StepWord make_step<StepWord>(const uint8_t* lds, const ScanArgs& a) {
-  return StepWord{lds,      reinterpret_cast<const uint32_t*>(lds + a.wd_t1), a.nclasses, a.wd_pb, a.wd_wc,
-                  a.wd_thr_e, a.wd_thr_r, a.wd_row, a.wd_tw};
-}
-template <>
 __device__ __forceinline__ StepTable make_step<StepTable>(const uint8_t* lds, const ScanArgs&) { return StepTable{lds}; }
 template <>
 __device__ __forceinline__ StepSheng8 make_step<StepSheng8>(const uint8_t* lds, const ScanArgs&) {
   return StepSheng8{reinterpret_cast<const uint2*>(lds)};
-}
-template <>
-__device__ __forceinline__ StepWide make_step<StepWide>(const uint8_t* lds, const ScanArgs& a) {
-  return StepWide{lds, reinterpret_cast<const uint16_t*>(lds + kWideClassBytes), a.wide, a.nclasses,
-                  a.hot_entries};
 }
 
 template <class Step>
@@ -564,27 +408,15 @@ struct Tune<StepTable> {
   static constexpr int C = DGREP_TABLE_CHUNK, E = DGREP_TABLE_SLOTS, B = DGREP_TABLE_BLOCK, S = 2;
 };
 template <>
-struct Tune<StepWide> {
-  static constexpr int C = DGREP_WIDE_CHUNK, E = DGREP_WIDE_SLOTS, B = DGREP_WIDE_BLOCK, S = 1;
-};
-template <>
 struct Tune<StepFilter> {
   static constexpr int C = DGREP_FILTER_CHUNK, E = DGREP_FILTER_SLOTS, B = DGREP_FILTER_BLOCK, S = 1;
 };
 static_assert(Tune<StepFilter>::C % Tune<StepFilter>::B == 0 && Tune<StepFilter>::C <= 32768, "bad filter chunk");
 template <uint32_t ESZ>
 struct Tune<StepPairT<ESZ>> {
-  static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = DGREP_PAIR_STREAMS;
+  static constexpr int C = DGREP_PAIR_CHUNK, E = DGREP_PAIR_SLOTS, B = DGREP_PAIR_BLOCK, S = 1;
 };
 static_assert(Tune<StepPair>::B == 64 || Tune<StepPair>::B == 128, "block must be 64 or 128 bytes");
-// Word (C3): as the pair stepper, one chunk per lane, 128-B blocks (run_block_word)
-#ifndef DGREP_WORD_SLOTS
-#define DGREP_WORD_SLOTS 16
-#endif
-template <>
-struct Tune<StepWord> {
-  static constexpr int C = 4096, E = DGREP_WORD_SLOTS, B = 128, S = 1;
-};
 static_assert(Tune<StepPair>::C % Tune<StepPair>::B == 0 && Tune<StepPair>::C <= 32768, "bad pair chunk");
 static_assert(Tune<StepSheng8>::B == 64 || Tune<StepSheng8>::B == 128, "block must be 64 or 128 bytes");
 static_assert(Tune<StepTable>::B == 64 || Tune<StepTable>::B == 128, "block must be 64 or 128 bytes");
@@ -601,8 +433,7 @@ static_assert(Tune<StepSheng8>::C % Tune<StepSheng8>::B == 0 && Tune<StepTable>:
 #endif
 constexpr int kMaxLaneChunk = DGREP_MAX_LANE_CHUNK;
 static_assert(kMaxLaneChunk <= 65536, "16-bit slot offsets and 23-bit tile-relative line indices");
-static_assert(Tune<StepSheng8>::C <= kMaxLaneChunk && Tune<StepTable>::C <= kMaxLaneChunk &&
-                  Tune<StepWide>::C <= kMaxLaneChunk,
+static_assert(Tune<StepSheng8>::C <= kMaxLaneChunk && Tune<StepTable>::C <= kMaxLaneChunk,
               "lane chunk above 64 KiB overflows the 16-bit LDS slot offsets");
 
 // chunks per lane: the table stepper runs two in lockstep while its table is
@@ -733,20 +564,6 @@ struct Emitter {
     if (r.nev - uint32_t(E) < spill_cap) spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);  // wraps below E
     r.nev += own ? 1u : 0u;
   }
-  // inner_flat run by EVERY lane of the wave (word_events_wave): count = the
-  // lane has this record; the others write to an unclaimed slot. The spill
-  // store, rare, behind a ballot branch.
-  __device__ __forceinline__ void inner_wave(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool count) const {
-    const uint32_t lw = q - start;
-    const uint32_t w0 = start | (rel << 16);
-    const uint32_t i = min(r.nev, uint32_t(E));
-    *reinterpret_cast<uint2*>(slots + 2u * i) = make_uint2(w0, lw);
-    const bool sp = count && r.nev >= uint32_t(E);
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(sp) != 0, 0)) {
-      if (sp && r.nev - uint32_t(E) < spill_cap) spill[r.nev - uint32_t(E)] = make_uint2(w0, lw);
-    }
-    r.nev += count ? 1u : 0u;
-  }
   __device__ __forceinline__ void inner(LaneRun& r, uint32_t q, uint32_t start, uint32_t rel, bool cand) const {
     const uint32_t lw = (q - start) | (cand ? kCandidateBit : 0u);
     if (DIRECT) {
@@ -777,6 +594,7 @@ struct Blk {
   bool past;        // block lies at or beyond the chunk end
   uint32_t nlrun;   // '\n' consumed by the lane so far (r.nl at block start + this block's)
   uint32_t lnl;     // the line the next byte belongs to, encoded (lnl_update); 0: not owned
+  uint32_t evb;     // DGREP_EV_PROBE 2: event bits shifted in per word
 };
 // Where the current line started, as ONE register per block: lnl = 8 * (q + 3 +
 // kLnlOff) for the last '\n' seen at block offset q. Word J with newline mask m
@@ -807,7 +625,7 @@ __device__ __forceinline__ uint32_t lnl_pos(uint32_t lnl) { return (lnl >> 3) - 
 // event path runs in ~27 % of words, and costs the Sheng stepper 1.8 % (C2,
 // profiles/r03/ablation/sentinel_c2.txt): a per-block init for a rare path.
 #ifndef DGREP_SENTINEL_KINDS
-#define DGREP_SENTINEL_KINDS ((1 << kStepPair) | (1 << kStepFilter) | (1 << kStepTable) | (1 << kStepWide) | (1 << kStepWord))
+#define DGREP_SENTINEL_KINDS ((1 << kStepPair) | (1 << kStepFilter) | (1 << kStepTable))
 #endif
 template <class Step>
 constexpr bool sentinel() {
@@ -818,8 +636,7 @@ constexpr bool sentinel() {
 template <class Step, bool DIRECT>
 constexpr bool flat_emit() {
   // (not Filter: its 1024 threads x 8 B dummy would not fit beside its 124 KiB image)
-  return !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepWord) &&
-         Tune<Step>::S == 1;
+  return !DIRECT && (Step::kKind == kStepSheng8 || Step::kKind == kStepPair) && Tune<Step>::S == 1;
 }
 
 // Everything a word step does after its four DFA steps s0..s3 (newline mask
@@ -993,39 +810,29 @@ __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
 #ifndef DGREP_EV_BALLOT
 #define DGREP_EV_BALLOT ((1 << kStepPair) | (1 << kStepFilter))
 #endif
-// The event fast path run by the whole wave once any lane has an event
-// (word_events, Emitter::inner_wave): selects instead of the nested exec-mask
-// regions of the single-'\n' test, the own test and the spill test. Needs
-// the flat emitter and the sentinel line start; no filter candidates.
-#ifndef DGREP_EV_WAVE
-#define DGREP_EV_WAVE 0
+#ifndef DGREP_EV_PROBE
+#define DGREP_EV_PROBE 0
 #endif
-template <class Step, bool DIRECT>
-constexpr bool ev_wave() {
-  return flat_emit<Step, DIRECT>() && sentinel<Step>() && Step::kKind != kStepFilter && Step::kKind != kStepWord &&
-         (((DGREP_EV_WAVE) >> Step::kKind) & 1);
-}
 template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
-  const bool ev = word_any(st, M, s0, s1, s2, s3);
-  if constexpr (ev_wave<Step, DIRECT>()) {
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
-      // the fast path by every lane, no exec-mask regions (see inner_wave):
-      // counted for an event word with one '\n', inside the chunk, owned
-      uint32_t t;
-      asm("v_ffbl_b32 %0, %1" : "=v"(t) : "v"(m));  // ffbl(0) = ~0: garbage for uncounted lanes
-      const uint32_t k = t >> 3;
-      const bool single = (m & (m - 1u)) == 0u;
-      const uint32_t start = uint32_t(b.pos) + (b.lnl >> 3) - (2u + kLnlOff);
-      emit.inner_wave(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, ev && single && !b.past && b.lnl != 0);
-      const bool gen = ev && !(single && !b.past);
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(gen) != 0, 0)) {
-        if (gen) word_emit_loop<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+  if constexpr (DGREP_EV_PROBE != 0 && Step::kKind == kStepPair && !DIRECT) {
+    // timing probes (wrong output): 1 no event test, 2 event bits shifted in
+    // without a branch, 3 neither events nor newline bookkeeping, 4 the ballot
+    // branch with a one-instruction body
+    if constexpr (DGREP_EV_PROBE == 2) b.evb = b.evb + b.evb + (word_any(st, M, s0, s1, s2, s3) ? 1u : 0u);
+    if constexpr (DGREP_EV_PROBE == 4) {
+      const bool ev = word_any(st, M, s0, s1, s2, s3);
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
+        if (ev) asm volatile("v_add_u32 %0, 1, %0" : "+v"(b.evb));
       }
     }
-  } else if constexpr (((DGREP_EV_BALLOT) >> Step::kKind) & 1) {
+    if constexpr (DGREP_EV_PROBE != 3) word_nl<J>(m, b);
+    return;
+  }
+  const bool ev = word_any(st, M, s0, s1, s2, s3);
+  if constexpr (((DGREP_EV_BALLOT) >> Step::kKind) & 1) {
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
       if (ev) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
     }
@@ -1035,30 +842,12 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
   word_nl<J>(m, b);
 }
 
-// StepWord: the events of word J (data x, states sp before it and se after
-// it). An event or recheck shows as se >= thr_e; a single '\n' inside the
-// chunk is the event (the shadow's meaning), anything else is recomputed byte
-// by byte from sp and takes word_emit's general loop.
-template <int J, int E, bool DIRECT>
-__device__ __forceinline__ void word_events_word(const StepWord& st, uint32_t M, uint32_t m, uint32_t x, uint32_t sp,
-                                                 uint32_t se, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit) {
-  if (__builtin_expect(se >= st.thr_e, 0)) {
-    if (!b.past && (m & (m - 1u)) == 0u) {
-      word_emit<J>(st, M, m, se, se, se, se, b, r, emit);  // its fast path
-    } else {
-      uint32_t s0, s1, s2, s3;
-      st.bytes4(sp, x, s0, s1, s2, s3);
-      word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);  // its general loop
-    }
-  }
-  word_nl<J>(m, b);
-}
-
 template <bool SENT>
 __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const LaneRun& r) {
   b.pos = pos;
   b.past = pos >= C;
   b.nlrun = r.nl;
+  b.evb = 0;
   // inside the chunk: r.prev_nl - pos >= -(C + 1) > -kLnlOff
   if constexpr (SENT)
     b.lnl = !r.seen ? 0u : b.past ? kLnlSeen : 8u * uint32_t(int32_t(r.prev_nl - int64_t(pos)) + int32_t(3u + kLnlOff));
@@ -1067,6 +856,7 @@ __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const
 }
 
 __device__ __forceinline__ void blk_finish(const Blk& b, uint32_t s, LaneRun& r) {
+  if constexpr (DGREP_EV_PROBE == 2 || DGREP_EV_PROBE == 4) asm volatile("" ::"v"(b.evb));
   r.s = s;
   r.nl = b.nlrun;
   if (b.lnl >= kLnlBase) {
@@ -1171,89 +961,6 @@ __device__ __forceinline__ void run_block_pipe(const Step& st, uint32_t M, const
   DG_WP(24) DG_WP(25) DG_WP(26) DG_WP(27) DG_WP(28) DG_WP(29) DG_WP(30) DG_WP(31)
 #undef DG_WP
   blk_finish(b, s, r);
-}
-
-// StepWord's lookahead, carried from block to block (see run_block_word).
-// Entering word J: f = word J's chain read (in flight); c1 = word J+1's column
-// bytes; a2/b2 = word J+2's pair entries (PA, PB); x3[4] = word J+3's byte
-// entries (UA, UB, UA, UB).
-struct WordPipe {
-  uint32_t f, c1, a2, b2;
-  uint32_t x3[4];
-  bool warm;
-};
-__device__ __forceinline__ void word_bytes_cls(const StepWord& st, uint32_t x, uint32_t (&c)[4]) {
-  c[0] = st.ua(x & 0xffu);
-  c[1] = st.ub((x >> 8) & 0xffu);
-  c[2] = st.ua((x >> 16) & 0xffu);
-  c[3] = st.ub(x >> 24);
-}
-
-// One block of StepWord: per word ONE dependent LDS read on the chain. Word
-// J's step, LDS reads completing in issue order:
-//   wait f (word J's state); issue word J+1's chain read (state + c1) FIRST;
-//   then the table levels, each from the level the previous step issued
-//   (complete a few LDS cycles after that step's chain read): word J+2's
-//   column (WC), word J+3's pair entries (PA, PB), word J+4's byte entries;
-//   then word J's events and newline bookkeeping, under the chain read.
-// Words past the block come from the next block's registers (nx).
-template <int BK, int E, bool DIRECT>
-__device__ __forceinline__ void run_block_word(const StepWord& st, uint32_t M, const uint4 (&v)[BK / 16],
-                                               const uint4 (&nx)[BK / 16], uint64_t pos, uint64_t C, LaneRun& r,
-                                               const Emitter<E, DIRECT>& emit, WordPipe& q) {
-  static_assert(BK == 128, "the word stepper's lookahead is laid out for 128-byte blocks");
-  Blk b;
-  blk_init<true>(b, pos, C, r);
-  constexpr int NW = BK / 4;
-  uint32_t w[NW + 4];
-#pragma unroll
-  for (int i = 0; i < BK / 16; ++i) {
-    w[4 * i + 0] = v[i].x;
-    w[4 * i + 1] = v[i].y;
-    w[4 * i + 2] = v[i].z;
-    w[4 * i + 3] = v[i].w;
-  }
-  w[NW + 0] = nx[0].x;
-  w[NW + 1] = nx[0].y;
-  w[NW + 2] = nx[0].z;
-  w[NW + 3] = nx[0].w;
-  if (!q.warm) {
-    // cold start (a lane's first block): the lookahead of words 0-3
-    const uint32_t c0 = st.prep(w[0]).col;
-    q.c1 = st.prep(w[1]).col;
-    uint32_t x2[4];
-    word_bytes_cls(st, w[2], x2);
-    q.a2 = st.pa(x2[0] + x2[1]);
-    q.b2 = st.pbv(x2[2] + x2[3]);
-    word_bytes_cls(st, w[3], q.x3);
-    q.f = st.step(r.s, c0);
-    q.warm = true;
-  }
-  uint32_t sp = r.s;
-#define DG_WW(J)                                                                          \
-  {                                                                                       \
-    const uint32_t sJ = q.f;                                                              \
-    q.f = st.step(sJ, q.c1); /* word J+1's chain read */                                 \
-    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
-    const uint32_t c2 = st.wcol(q.a2 + q.b2);                                             \
-    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
-    const uint32_t a3 = st.pa(q.x3[0] + q.x3[1]), b3 = st.pbv(q.x3[2] + q.x3[3]);         \
-    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
-    word_bytes_cls(st, w[(J) + 4], q.x3);                                                 \
-    __builtin_amdgcn_sched_barrier(kSchedNoDs);                                           \
-    const uint32_t m = nl_mask(w[J]);                                                     \
-    word_events_word<J>(st, M, m, w[J], sp, sJ, b, r, emit);                              \
-    sp = sJ;                                                                              \
-    q.c1 = c2;                                                                            \
-    q.a2 = a3;                                                                            \
-    q.b2 = b3;                                                                            \
-  }
-  DG_WW(0) DG_WW(1) DG_WW(2) DG_WW(3) DG_WW(4) DG_WW(5) DG_WW(6) DG_WW(7)
-  DG_WW(8) DG_WW(9) DG_WW(10) DG_WW(11) DG_WW(12) DG_WW(13) DG_WW(14) DG_WW(15)
-  DG_WW(16) DG_WW(17) DG_WW(18) DG_WW(19) DG_WW(20) DG_WW(21) DG_WW(22) DG_WW(23)
-  DG_WW(24) DG_WW(25) DG_WW(26) DG_WW(27) DG_WW(28) DG_WW(29) DG_WW(30) DG_WW(31)
-#undef DG_WW
-  blk_finish(b, sp, r);
 }
 
 template <int BK, bool MAP, class Step, int E, bool DIRECT>
@@ -1388,7 +1095,7 @@ __device__ __forceinline__ void lane_init(const ScanArgs& a, uint64_t cs, LaneRu
 template <class Step, bool DIRECT>
 constexpr bool track_long() {
   return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepTable ||
-          Step::kKind == kStepWord || (Step::kKind == kStepFilter && DGREP_FILTER_PARK)) &&
+          (Step::kKind == kStepFilter && DGREP_FILTER_PARK)) &&
          !DIRECT;
 }
 // the parked state as an index of ScanArgs::pend_states (stepper encoding ->
@@ -1397,7 +1104,6 @@ template <class Step>
 __device__ __forceinline__ uint32_t park_index(const ScanArgs& a, uint32_t s) {
   if constexpr (Step::kKind == kStepSheng8) return s & 0xffu;
   else if constexpr (Step::kKind == kStepPair) return (s - Step::kT2) / a.pair_div;
-  else if constexpr (Step::kKind == kStepWord) return (s - a.wd_tw) / a.wd_row;
   else if constexpr (Step::kKind == kStepFilter) return 0;  // re-run from the line start
   else return s;
 }
@@ -1513,12 +1219,8 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
   const bool maps = kMap && emit.cmap != nullptr;
   if (maps && pos0 == 0) *emit.mapsl = make_uint2(0x03020100u, 0x07060504u);  // identity
   if (pos0 + BK <= avail) load_block<BK>(A, p + pos0);
-  WordPipe wp;  // StepWord: the lookahead carried from block to block
-  wp.warm = false;
 #define DG_STEP(V, NX)                                                                     \
-  if constexpr (Step::kKind == kStepWord)                                                  \
-    run_block_word<BK>(st, M, V, NX, pos, uint64_t(C), r, emit, wp);                       \
-  else if (kMap && __ballot(maps && r.nl == 0u && pos >= kLazyMapBytes && pos < uint64_t(C)) != 0) \
+  if (kMap && __ballot(maps && r.nl == 0u && pos >= kLazyMapBytes && pos < uint64_t(C)) != 0) \
     run_block<BK, kMap>(st, M, V, pos, uint64_t(C), r, emit);                              \
   else                                                                                     \
     run_block<BK, false>(st, M, V, pos, uint64_t(C), r, emit);
@@ -1570,9 +1272,12 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
     // The blocks inside the chunk of a wave whose lanes all hold C + BK bytes:
     // no lane leaves before C, so this loop's trip count is wave-uniform --
     // scalar loop control, none of the per-lane exit masks (and their SALU
-    // merges at every latch) of the loop below, which then runs only past C.
+    // merges at every latch) of the loop below, which then runs only from the
+    // last whole pair of blocks before C on. It steps two blocks per trip and
+    // never past C: a forced chunk of an odd number of blocks (4224 B) leaves
+    // its last block to the loop below, which takes the pos == C snapshot.
     if (pos < uint64_t(C) && __all(avail >= uint64_t(C) + BK)) {
-      do {
+      while (pos + 2 * BK <= uint64_t(C)) {
         if constexpr (kMap && kLazyMapBytes != 0) {
           if (maps && pos == kLazyMapBytes) {
             if (r.nl != 0u)
@@ -1595,7 +1300,7 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
         load_block<BK>(A, p + pos + BK);
         DG_STEP(B, A)
         pos += BK;
-      } while (pos < uint64_t(C));
+      }
     }
   }
   for (;;) {
@@ -1662,8 +1367,7 @@ __device__ __forceinline__ void run_lane2(const ScanArgs& a, const Step& st, uin
 // (run_lane2) is compiled for Tune::C.
 template <class Step, int TBL>
 constexpr bool adaptive_chunk() {
-  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepFilter ||
-          Step::kKind == kStepWord) &&
+  return (Step::kKind == kStepSheng8 || Step::kKind == kStepPair || Step::kKind == kStepFilter) &&
          streams_of<Step, TBL>() == 1;
 }
 template <class Step, int TBL>
@@ -1709,9 +1413,8 @@ template <class Step>
 constexpr int waves_per_simd() {
   return Step::kKind == kStepSheng8  ? DGREP_SHENG_WAVES
          : Step::kKind == kStepTable ? DGREP_TABLE_WAVES
-         : Step::kKind == kStepPair || Step::kKind == kStepWord ? DGREP_PAIR_WAVES
-                                     : Step::kKind == kStepFilter ? kFilterThreads / 256
-                                                                  : kWideThreads / 256;  // one workgroup per CU
+         : Step::kKind == kStepPair  ? DGREP_PAIR_WAVES
+                                     : kFilterThreads / 256;  // one workgroup per CU
 }
 
 // the next tile for this wave: waves + (claims so far), wave-uniform
@@ -1719,11 +1422,6 @@ constexpr int waves_per_simd() {
 #ifndef DGREP_DYNAMIC_TILES
 #define DGREP_DYNAMIC_TILES 1
 #endif
-__device__ __forceinline__ uint64_t wave_sum_u64_(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
 __device__ __forceinline__ uint64_t claim_tile(const ScanArgs& a) {
   uint64_t c = 0;
   if ((threadIdx.x & 63u) == 0) c = atomicAdd(a.tile_next, 1ull);
@@ -1731,136 +1429,11 @@ __device__ __forceinline__ uint64_t claim_tile(const ScanArgs& a) {
   return (uint64_t(hi) << 32) | lo;
 }
 __device__ __forceinline__ uint64_t next_tile(const ScanArgs& a, uint64_t t, uint64_t waves) {
-  // in-scan ordering: EVERY tile is claimed (see order_tile), none by index
-  if (a.out_line) return claim_tile(a);
   if (!DGREP_DYNAMIC_TILES) return t + waves;
   return waves + claim_tile(a);
 }
-__device__ __forceinline__ uint64_t first_tile(const ScanArgs& a, int tid, int NT) {
-  if (a.out_line) return claim_tile(a);
+__device__ __forceinline__ uint64_t first_tile(int tid, int NT) {
   return uint64_t(blockIdx.x) * uint64_t(NT / 64) + uint64_t(tid >> 6);
-}
-
-// ---- in-scan ordering (single pass) -----------------------------------------
-// Without it, two passes after the scan place the tiles' staged lines
-// (tile_block_sum_kernel, order_lines_kernel: C3's 21.4 M records, 4 % of a
-// step). With ScanArgs::out_line set, each wave places a tile's lines itself:
-// at a tile's end it publishes the tile's aggregate (records, '\n'), and after
-// its NEXT tile (or at its end) it finds the tile's exclusive prefix by a
-// decoupled look-back over its predecessors' published aggregates / inclusive
-// prefixes, publishes its own inclusive prefix and copies the tile's staged
-// lines to their final slots -- while other waves still scan, so the copy
-// overlaps the scan's HBM stream. Deadlock-free: every tile is claimed from
-// the counter by a running wave (first_tile), a wave publishes a tile's
-// aggregate before it waits on anything, and the look-back waits only for
-// tiles claimed before the one it places.
-// Entries carry the launch's epoch (ScanArgs::epoch, never 0) in bits 48-63:
-// an entry of an earlier launch reads as not yet published, so nothing is
-// cleared between launches (the arrays are zeroed once, when allocated).
-//   agg[t]    = epoch | nl << 24 | count   (a tile's '\n' and records: < 2^23 each)
-//   incl_c[t] = epoch | records of tiles 0..t   (48 bits)
-//   incl_l[t] = epoch | '\n' of tiles 0..t      (48 bits)
-constexpr uint64_t kEpochShift = 48;
-constexpr uint64_t kVal48 = (1ull << kEpochShift) - 1ull;
-__device__ __forceinline__ uint64_t ld_dev(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_dev(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// the exclusive prefix (records, '\n') of tile t, by the whole wave
-__device__ __forceinline__ void tile_prefix(const ScanArgs& a, uint64_t t, uint64_t& pc, uint64_t& pl) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t ep = uint64_t(a.epoch) << kEpochShift;
-  pc = 0;
-  pl = 0;
-  int64_t j = int64_t(t) - 1;  // the window is tiles j - 63 .. j, lane l at j - l
-  while (j >= 0) {
-    const int64_t jj = j - int64_t(lane);
-    const bool in = jj >= 0;
-    uint64_t ic = 0, il = 0, ag = 0;
-    bool vinc = false, vagg = false;
-    if (in) {
-      ic = ld_dev(a.incl_c + jj);
-      il = ld_dev(a.incl_l + jj);
-      vinc = (ic & ~kVal48) == ep && (il & ~kVal48) == ep;
-      if (!vinc) {
-        ag = ld_dev(a.agg + jj);
-        vagg = (ag & ~kVal48) == ep;
-      }
-    }
-    // the nearest predecessor with an inclusive prefix ends the walk; every
-    // tile after it needs its aggregate
-    const uint64_t minc = __ballot(in && vinc);
-    const uint32_t stop = minc ? uint32_t(__builtin_ctzll(minc)) : 64u;
-    const bool need = in && lane < stop;
-    if (__ballot(need && !vagg)) {
-      __builtin_amdgcn_s_sleep(4);  // a predecessor still scans: read the window again
-      continue;
-    }
-    uint64_t c = 0, l = 0;
-    if (need) {
-      c = ag & 0xffffffull;
-      l = (ag >> 24) & 0xffffffull;
-    } else if (in && lane == stop) {
-      c = ic & kVal48;
-      l = il & kVal48;
-    }
-    pc += wave_sum_u64_(c);
-    pl += wave_sum_u64_(l);
-    if (stop < 64u) break;
-    j -= 64;
-  }
-}
-
-// A tile scanned by this wave, waiting to be placed (wave-uniform).
-struct HeldTile {
-  uint64_t t;      // tile index (kNoTile: none)
-  uint64_t base;   // its first staged line
-  uint32_t count;  // its records
-  uint32_t nl;     // its '\n'
-};
-constexpr uint64_t kNoTile = ~0ull;
-
-__device__ __forceinline__ void publish_agg(const ScanArgs& a, uint64_t t, uint32_t count, uint32_t nl) {
-  if ((threadIdx.x & 63u) == 0)
-    st_dev(a.agg + t, (uint64_t(a.epoch) << kEpochShift) | (uint64_t(nl) << 24) | uint64_t(count));
-}
-
-// Place a held tile: its prefix, its inclusive prefix published, its staged
-// lines copied to their final SoA slots (line_no = 1 + '\n' before the line).
-__device__ __forceinline__ void order_tile(const ScanArgs& a, const HeldTile& h) {
-  uint64_t pc, pl;
-  tile_prefix(a, h.t, pc, pl);
-  const uint32_t lane = threadIdx.x & 63u;
-  if (lane == 0) {
-    const uint64_t ep = uint64_t(a.epoch) << kEpochShift;
-    st_dev(a.incl_l + h.t, ep | ((pl + h.nl) & kVal48));
-    st_dev(a.incl_c + h.t, ep | ((pc + h.count) & kVal48));
-  }
-  // the staged lines were written by this wave a tile ago
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const uint64_t lb = pl + 1;
-  constexpr uint32_t U = 4;  // records per lane in flight
-  for (uint32_t k0 = 0; k0 < h.count; k0 += 64u * U) {
-    StagedLine L[U];
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t k = k0 + u * 64u + lane;
-      if (k < h.count && h.base + k < a.capacity) L[u] = a.staging[h.base + k];
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t k = k0 + u * 64u + lane;
-      const uint64_t dst = pc + k;
-      if (k < h.count && h.base + k < a.capacity && dst < a.out_cap) {
-        a.out_line[dst] = lb + staged_rel(L[u]);
-        a.out_start[dst] = L[u].start;
-        a.out_len[dst] = staged_len(L[u]);
-      }
-    }
-  }
 }
 
 // One wave = one tile of 64 chunks. Waves never synchronise with each other:
@@ -1892,8 +1465,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
   // older waves): with a static stride the youngest waves set the kernel's
   // end. Same box, C2 pattern: 12 / 18 / 32 GiB splits ran 9 % below 16 GiB,
   // whose 2.67 rounds happened to give the young waves one tile less.
-  HeldTile held{kNoTile, 0, 0, 0};  // in-scan ordering: the tile to place after this one
-  for (uint64_t t = first_tile(a, tid, NT); t < a.ntiles; t = next_tile(a, t, waves)) {
+  for (uint64_t t = first_tile(tid, NT); t < a.ntiles; t = next_tile(a, t, waves)) {
     uint64_t cs[S];
     LaneRun r[S];
     uint32_t nlc[S];
@@ -1965,7 +1537,6 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
       ti.nl = nl_tot;
       a.tiles[t] = ti;
     }
-    if (a.out_line) publish_agg(a, t, ev_tot, nl_tot);
     base = (uint64_t(uint32_t(__shfl(uint32_t(base >> 32), 0, 64))) << 32) | uint32_t(__shfl(uint32_t(base), 0, 64));
 #pragma unroll
     for (int k = 0; k < S && ev_tot != 0; ++k) {  // ev_tot: wave-uniform
@@ -2026,14 +1597,7 @@ __global__ __launch_bounds__(NT, waves_per_simd<Step>()) void scan_dfa8_kernel(S
         }
       }
     }
-    if (a.out_line) {
-      // place the tile scanned before this one (its predecessors are done by
-      // now, nearly always), then hold this one
-      if (held.t != kNoTile) order_tile(a, held);
-      held = HeldTile{t, base, ev_tot, nl_tot};
-    }
   }
-  if (held.t != kNoTile) order_tile(a, held);
 }
 
 // Lanes that owned more matching lines than their LDS slots are re-run here,
@@ -2824,13 +2388,13 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
     d.xr = reinterpret_cast<const uint2*>(lbuf + la.xr_off);
     d.xh = la.x_hot;
   }
-  // one DFA step on scaled class ce: the entry's LDS address in one v_mad, read
-  // unconditionally (past the resident rows it reads the extra rows, the
-  // records or nothing: LDS is bounds-checked), the cold path behind a ballot
+  // one DFA step on scaled class ce: the entry's LDS address in one v_mad,
+  // clamped to the resident rows (one v_min) and read unconditionally; a state
+  // past them takes the cold path behind a ballot, which replaces the value
   const uint32_t KE = la.nclasses * uint32_t(sizeof(E)), hot_end = hot_n * uint32_t(sizeof(E));
   auto step_c = [&](uint32_t s, uint32_t ce) __attribute__((always_inline)) -> uint32_t {
     const uint32_t ad = __umul24(s, KE) + ce;
-    uint32_t t = uint32_t(*reinterpret_cast<const E*>(lbuf + ad));
+    uint32_t t = uint32_t(*reinterpret_cast<const E*>(lbuf + min(ad, hot_end - uint32_t(sizeof(E)))));
     const bool k = ad >= hot_end;
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(k) != 0, 0)) {
       if (k) t = d.cold(s, ce / uint32_t(sizeof(E)), ad / uint32_t(sizeof(E)));
@@ -2971,9 +2535,6 @@ __global__ __launch_bounds__(256) void tile_block_sum_kernel(const TileInfo* til
 #endif
 constexpr uint32_t kOrderUnroll = DGREP_ORDER_UNROLL;
 // streaming (nontemporal) stores for the three output arrays, for A/B
-#ifndef DGREP_ORDER_NT
-#define DGREP_ORDER_NT 0
-#endif
 __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles, const StagedLine* staging,
                                                           uint64_t ntiles, const uint64_t* bsum_c,
                                                           const uint64_t* bsum_l, uint64_t staging_cap,
@@ -3014,15 +2575,9 @@ __global__ __launch_bounds__(256) void order_lines_kernel(const TileInfo* tiles,
       for (uint32_t u = 0; u < kOrderUnroll; ++u) {
         const uint64_t dst = o + k0 + u * 64u + lane;
         if (ok[u]) {
-#if DGREP_ORDER_NT
-          __builtin_nontemporal_store(lb + staged_rel(L[u]), line_no + dst);
-          __builtin_nontemporal_store(L[u].start, start + dst);
-          __builtin_nontemporal_store(staged_len(L[u]), len + dst);
-#else
           line_no[dst] = lb + staged_rel(L[u]);
           start[dst] = L[u].start;
           len[dst] = staged_len(L[u]);
-#endif
         }
       }
     }
@@ -3041,7 +2596,7 @@ uint32_t scan_max_lane_chunk() { return uint32_t(kMaxLaneChunk); }
 namespace {
 template <class Step>
 constexpr int threads_of() {
-  return Step::kKind == kStepWide ? kWideThreads : Step::kKind == kStepFilter ? kFilterThreads : kScanThreads;
+  return Step::kKind == kStepFilter ? kFilterThreads : kScanThreads;
 }
 template <class Step, int TBL>
 hipError_t launch_t(const ScanArgs& a, int grid, hipStream_t stream) {
@@ -3102,11 +2657,6 @@ static_assert(kShengMaxChunk <= uint64_t(kMaxLaneChunk), "adaptive chunk above t
 // 32 KiB beat 16 KiB (profiles/r04/ablation/chunk_dyn.txt).
 // The filter stops at 32 KiB (64 KiB chunks were measured on the Sheng
 // stepper's access pattern only).
-// The word stepper starts from the pair stepper's 8 KiB (same slots, same
-// event density).
-#ifndef DGREP_WORD_MAX_CHUNK
-#define DGREP_WORD_MAX_CHUNK 8192
-#endif
 #ifndef DGREP_FILTER_MAX_CHUNK
 #define DGREP_FILTER_MAX_CHUNK 32768
 #endif
@@ -3149,7 +2699,6 @@ struct TileOp {
       c = force ? uint64_t(force)
                 : adaptive_chunk_bytes(n, resident_blocks * uint64_t(threads_of<S>() / 64), c, dens_cap,
                                        S::kKind == kStepPair     ? DGREP_PAIR_MAX_CHUNK
-                                       : S::kKind == kStepWord   ? DGREP_WORD_MAX_CHUNK
                                        : S::kKind == kStepFilter ? DGREP_FILTER_MAX_CHUNK
                                                                  : kShengMaxChunk,
                                        // the filter keeps 32 KiB at 2 tiles per wave (C4: 16 KiB -1.5 %)
@@ -3187,10 +2736,6 @@ hipError_t part_sheng(int, uint32_t, const Op& op) {
 }
 template <class Op>
 hipError_t part_pair(int kind, uint32_t table_bytes, const Op& op) {
-  if ((kind & ~kKindW32) == kStepWord) {
-    if (table_bytes <= 8192) return op.template run<StepWord, 8192>();
-    return op.template run<StepWord, int(kWordMaxImage)>();
-  }
   if (kind & kKindW32) {
     if (table_bytes <= 8192) return op.template run<StepPair, 8192>();
     return op.template run<StepPair, int(kPairW32MaxImage)>();  // C3 (15.6 KiB)
@@ -3208,7 +2753,6 @@ hipError_t part_table(int, uint32_t table_bytes, const Op& op) {
 }
 template <class Op>
 hipError_t part_big(int kind, uint32_t, const Op& op) {
-  if (kind == kStepWide) return op.template run<StepWide, int(kWideClassBytes + kWideHotBytes)>();
   return op.template run<StepFilter, int(kFilterImageBytes)>();
 }
 // explicit instantiations in their part, extern elsewhere
@@ -3244,8 +2788,8 @@ template <class Op>
 hipError_t dispatch(int kind, uint32_t table_bytes, const Op& op) {
   const int k = kind & ~kKindW32;
   if (k == kStepSheng8) return part_sheng(k, table_bytes, op);
-  if (k == kStepPair || k == kStepWord) return part_pair(kind, table_bytes, op);
-  if (k == kStepWide || k == kStepFilter) return part_big(k, table_bytes, op);
+  if (k == kStepPair) return part_pair(kind, table_bytes, op);
+  if (k == kStepFilter) return part_big(k, table_bytes, op);
   return part_table(k, table_bytes, op);
 }
 }  // namespace scan_ops
@@ -3261,7 +2805,7 @@ uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t re
                  TileOp{&b, chunk, waves_per_block, n, resident_blocks, force, density, slots, spill_per_lane});
   *threads = *waves_per_block * 64;
   const int k = kind & ~kKindW32;
-  *spills = k == kStepSheng8 || k == kStepPair || k == kStepFilter || k == kStepWord;
+  *spills = k == kStepSheng8 || k == kStepPair || k == kStepFilter;
   return b;
 }
 hipError_t scan_dfa_occupancy(int kind, uint32_t table_bytes, int* blocks_per_cu) {

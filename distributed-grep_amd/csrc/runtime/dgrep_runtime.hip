@@ -31,16 +31,7 @@
 #define DGREP_SHENG_MAX_STATES 8
 #endif
 // DFAs above the Sheng limit whose two-byte table fits in LDS use the pair
-// stepper (0: they use the u8 table / wide steppers as before)
-// the word stepper (one lookup per 4 bytes) as the default for > 8-state DFAs
-// whose word tables fit (A/B knob). Off: measured slower than the pipelined
-// pair stepper on C3, same box (r05): kernel 0.507-0.512 vs 0.543 of HBM peak
-// -- its eight LDS reads per word (four byte classes, two pair classes, the
-// word class, the chain) cost more than the one chain read it saves. Forced
-// with dgrep_set_stepper(ctx, 5, 0).
-#ifndef DGREP_WORD_ENABLE
-#define DGREP_WORD_ENABLE 0
-#endif
+// stepper (0: they use the u8 table stepper)
 #ifndef DGREP_PAIR_ENABLE
 #define DGREP_PAIR_ENABLE 1
 #endif
@@ -62,15 +53,6 @@
 #ifndef DGREP_SHENG_MAPS
 #define DGREP_SHENG_MAPS 1
 #endif
-// A/B knob (off): the scan kernel places the lines itself (in-scan ordering,
-// scan_dfa.hip order_tile) instead of the two ordering passes after it,
-// whenever the speculative ordering applies (not the filter). Measured slower
-// on MI355X, same box (r05): C3 step 4.340 -> 4.357 ms, C2 3.380 -> 3.412 ms --
-// the placement added its time to the scan kernel's instead of hiding under it.
-#ifndef DGREP_SCAN_ORDER
-#define DGREP_SCAN_ORDER 0
-#endif
-
 namespace dgrep {
 // scan_dfa.hip
 uint64_t scan_tile_bytes(int kind, uint32_t table_bytes, uint64_t n, uint64_t resident_blocks, uint32_t force,
@@ -101,11 +83,6 @@ using namespace dgrep;
 constexpr size_t kCounters = 8;
 
 // StepPair image offsets and thresholds (see StepPair in scan_dfa.hip)
-// the word stepper's LDS offsets and thresholds (build_word_image)
-struct WordArgs {
-  uint32_t pb, wc, tw, t1, row, thr_e, thr_r;
-  uint32_t W, P;
-};
 struct PairArgs {
   uint32_t t1 = 0, thr = 0, div = 0, w32 = 0;
 };
@@ -123,16 +100,14 @@ struct dgrep_ctx {
   bool empty_line_matches = false;
   uint8_t* d_table = nullptr;  // stepper image (see dgrep_load_dfa)
   uint32_t table_bytes = 0;
-  uint16_t* d_wide = nullptr;  // kStepWide: the whole u16 [state][class] table
-  uint32_t nclasses = 0, hot_entries = 0;
-  // dgrep_set_stepper: force a stepper (0 auto, 1 wide, 2 u8 table, 3 pair, 4 filter) /
-  // cap the wide stepper's LDS rows (tests, tuning)
+  uint32_t nclasses = 0;
+  // dgrep_set_stepper: force a stepper (0 auto, 2 u8 table, 3 pair, 4 filter) /
+  // cap the filter stepper's LDS rows (tests, tuning)
   int force_stepper = 0;
-  uint32_t wide_hot_rows_cap = UINT32_MAX;
+  uint32_t filter_rows_cap = UINT32_MAX;
   uint32_t lane_chunk = 0;  // dgrep_set_lane_chunk (0 = adaptive)
   int step_kind = kStepTable;
   PairArgs pair_args;
-  WordArgs word_args{};
   // kStepFilter: CAND_END (premultiplied), and the whole DFA for verify_kernel
   uint32_t cand_end = UINT32_MAX;
   void* d_full = nullptr;      // [nstates][nclasses], the blob's ids: u16, or u32 above 65535 states
@@ -154,11 +129,6 @@ struct dgrep_ctx {
   uint64_t tiles_cap = 0, off_cap = 0, lb_cap = 0;
   StagedLine* d_staging = nullptr;
   uint64_t staging_cap = 0;
-  // in-scan ordering (ScanArgs::agg / incl_c / incl_l, 3 x order_cap entries,
-  // zeroed when allocated) and the epoch of the last launch (16 bits, never 0)
-  uint64_t* d_order = nullptr;
-  uint64_t order_cap = 0;
-  uint32_t epoch = 0;
   // device counters: [0] staging append counter, [1] overflow lanes, [2] parked
   // lines, [3] dropped candidates, [4] claimed tiles
   unsigned long long* d_counters = nullptr;
@@ -271,6 +241,16 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
   return DGREP_OK;
 }
 
+// Host wait per scan (scan_resident): block on the scan kernel's end event,
+// then poll the stream for the short tail (ordering passes, the 32-B count
+// copy) for at most DGREP_SYNC_SPIN_US microseconds before a blocking wait.
+// The poll holds one host core per rank busy for that tail (C3: ~0.16 ms per
+// scan, C2: ~0.05 ms); the blocking wait alone returned tens of µs after the
+// copy (profiles/r05/ablation/sync_spin.txt). 0: always the blocking wait.
+#ifndef DGREP_SYNC_SPIN_US
+#define DGREP_SYNC_SPIN_US 1000
+#endif
+
 // The LDS image through which long_dfa_seg_kernel and verify_kernel read a
 // whole u16 DFA F ([S][K], breadth-first ids) with no HBM access on the chain:
 // rows [0, H) whole; then one DfaXRec (scan_common.h) for each state in
@@ -282,9 +262,6 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 // records at *xr_off (8-aligned). H is the most rows that leave room for
 // everything within `budget`; false if even 64 rows do not (the kernels then
 // keep the first rows and read the rest from HBM).
-#ifndef DGREP_SYNC_SPIN
-#define DGREP_SYNC_SPIN 1
-#endif
 #ifndef DGREP_LONG_XREC
 #define DGREP_LONG_XREC 1
 #endif
@@ -338,7 +315,7 @@ static bool build_ximg(const uint16_t* F, uint32_t S, uint32_t K, uint32_t budge
 }
 
 // The pair stepper's LDS image (StepPair, scan_dfa.hip) from the blob's DFA:
-// UA, UB u32 [256] (byte -> column offsets), T2 u32 (u16 if the image exceeds 16 KiB) [S'][K][K] at kPairT2 (two
+// C u8 [256] (byte -> esz class), T2 u32 (u16 if the image exceeds 16 KiB) [S'][K][K] at kPairT2 (two
 // bytes per lookup), T1 u16 [S'][K] (single bytes); states premultiplied to
 // their T2 row's LDS address (kPairT2 + id * 2K^2). S' = S + shadows: a pair whose FIRST byte is a '\n'
 // entering start_m hides that event in the state between its bytes, so it
@@ -389,8 +366,6 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   const uint32_t thr_id = S - 1;
   auto premul = [&](uint32_t i) { return uint16_t(kPairT2 + uint64_t(i) * row); };
   img->assign(end, 0);
-  uint32_t* ua = reinterpret_cast<uint32_t*>(img->data());
-  uint32_t* ub = reinterpret_cast<uint32_t*>(img->data() + 1024);
   uint8_t* const t2 = img->data() + kPairT2;
   uint16_t* t1 = reinterpret_cast<uint16_t*>(img->data() + t1_off);
   for (uint32_t i = 0; i < Sp; ++i) {
@@ -412,16 +387,9 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
       }
     }
   }
-  for (int b = 0; b < 256; ++b) {
-    const uint32_t c = h.byte_class[b];
-    ua[b] = esz * K * c;
-    ub[b] = esz * c;
-  }
-  if (DGREP_PAIR_U8) {
-    // one u8 table C[b] = esz class(b) at LDS 0 (over UA); esz (K - 1) < 256
-    if (esz * (K - 1u) > 255u) return false;
-    for (int b = 0; b < 256; ++b) img->data()[b] = uint8_t(esz * h.byte_class[b]);
-  }
+  // one u8 table C[b] = esz class(b) at LDS 0; esz (K - 1) < 256
+  if (esz * (K - 1u) > 255u) return false;
+  for (int b = 0; b < 256; ++b) img->data()[b] = uint8_t(esz * h.byte_class[b]);
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
   *orig_out = orig;  // pair state index -> blob state (a shadow -> the state it copies)
@@ -429,126 +397,6 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
   pa->thr = premul(thr_id);
   pa->div = uint32_t(row);
   pa->w32 = esz == 4 ? 1u : 0u;
-  return true;
-}
-
-// The word stepper's LDS image (StepWord, scan_dfa.hip): the DFA's effect of
-// every 4-byte word of byte classes (K^4 of them) as a function on the states,
-// extended by the event rule -- a word whose single '\n' enters start_m before
-// its last byte leads to an EVENT shadow of the state it ends in, a word with
-// two or more '\n' to a RECHECK shadow -- numbered into W word classes; pair
-// classes (pairs of byte classes equivalent in either half of every word) make
-// the word class a two-level lookup WC[PA(b0, b1) + PB(b2, b3)]. Ids: the
-// states other than start_m, the event shadows, start_m, the recheck shadows;
-// u32 entries, states premultiplied to their TW row's address. Returns false
-// if the DFA does not fit (kWordMaxImage bytes, K <= 32, S <= 255).
-bool build_word_image(const dgrep_blob_header& h, const uint32_t* trans, std::vector<uint8_t>* img, uint32_t* start,
-                      uint32_t* start_m, WordArgs* wa, std::vector<uint32_t>* orig_out) {
-  const uint32_t S = h.nstates, K = h.nclasses, M = h.start_m;
-  const uint32_t cn = h.byte_class[uint8_t('\n')];
-  if (K > 32 || S > 255 || S < 2) return false;
-  const uint64_t K2 = uint64_t(K) * K, K4 = K2 * K2;
-  if (K4 * S > (uint64_t(1) << 24)) return false;
-  auto T = [&](uint32_t s, uint32_t c) { return trans[size_t(s) * K + c]; };
-  // per quad of classes and start state: x (plain), S + x (event shadow of x),
-  // 2 S + x (recheck shadow of x)
-  std::vector<uint32_t> F(size_t(K4) * S);
-  for (uint64_t q = 0; q < K4; ++q) {
-    const uint32_t c[4] = {uint32_t(q / (K2 * K)), uint32_t(q / K2 % K), uint32_t(q / K % K), uint32_t(q % K)};
-    const int nl = int(c[0] == cn) + int(c[1] == cn) + int(c[2] == cn) + int(c[3] == cn);
-    for (uint32_t s = 0; s < S; ++s) {
-      uint32_t x = s;
-      bool ev = false;
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t y = T(x, c[k]);
-        if (c[k] == cn && y == M && k < 3) ev = true;
-        x = y;
-      }
-      F[size_t(q) * S + s] = nl >= 2 ? 2 * S + x : (nl == 1 && ev ? S + x : x);
-    }
-  }
-  // word classes
-  std::map<std::vector<uint32_t>, uint32_t> wid;
-  std::vector<uint32_t> wq(K4), wrep;
-  for (uint64_t q = 0; q < K4; ++q) {
-    std::vector<uint32_t> f(F.begin() + size_t(q) * S, F.begin() + size_t(q + 1) * S);
-    auto it = wid.find(f);
-    if (it == wid.end()) {
-      it = wid.emplace(std::move(f), uint32_t(wrep.size())).first;
-      wrep.push_back(uint32_t(q));
-    }
-    wq[q] = it->second;
-  }
-  const uint32_t W = uint32_t(wrep.size());
-  // pair classes: pairs with the same word class in the first and in the
-  // second half of every word
-  std::map<std::vector<uint32_t>, uint32_t> pid;
-  std::vector<uint32_t> pc(K2);
-  for (uint64_t x = 0; x < K2; ++x) {
-    std::vector<uint32_t> sig(2 * K2);
-    for (uint64_t z = 0; z < K2; ++z) {
-      sig[z] = wq[x * K2 + z];
-      sig[K2 + z] = wq[z * K2 + x];
-    }
-    auto it = pid.emplace(std::move(sig), uint32_t(pid.size())).first;
-    pc[x] = it->second;
-  }
-  const uint32_t P = uint32_t(pid.size());
-  // ids
-  std::vector<uint8_t> is_e(S, 0), is_r(S, 0);
-  for (uint32_t v : F) {
-    if (v >= 2 * S) is_r[v - 2 * S] = 1;
-    else if (v >= S) is_e[v - S] = 1;
-  }
-  std::vector<uint32_t> id(S), eid(S, UINT32_MAX), rid(S, UINT32_MAX), orig;
-  for (uint32_t x = 0; x < S; ++x)
-    if (x != M) { id[x] = uint32_t(orig.size()); orig.push_back(x); }
-  const uint32_t first_e = uint32_t(orig.size());
-  for (uint32_t x = 0; x < S; ++x)
-    if (is_e[x]) { eid[x] = uint32_t(orig.size()); orig.push_back(x); }
-  id[M] = uint32_t(orig.size());
-  orig.push_back(M);
-  const uint32_t first_r = uint32_t(orig.size());
-  for (uint32_t x = 0; x < S; ++x)
-    if (is_r[x]) { rid[x] = uint32_t(orig.size()); orig.push_back(x); }
-  const uint32_t Sp = uint32_t(orig.size());
-  // layout (bytes)
-  const uint32_t pa = kWordPA, pb = pa + 4 * uint32_t(K2), wc = pb + 4 * uint32_t(K2);
-  const uint32_t tw = (wc + 4 * P * P + 15) & ~15u;
-  const uint32_t row = 4 * (W | 1u);  // an odd number of dwords: same column, different banks
-  const uint64_t t1 = (uint64_t(tw) + uint64_t(row) * Sp + 15) & ~uint64_t(15);
-  const uint64_t end = (t1 + 4ull * Sp * K + 15) & ~uint64_t(15);
-  if (end > kWordMaxImage) return false;
-  img->assign(end, 0);
-  auto put = [&](uint64_t off, uint32_t v) { memcpy(img->data() + off, &v, 4); };
-  auto premul = [&](uint32_t i) { return tw + i * row; };
-  auto code_id = [&](uint32_t v) { return v >= 2 * S ? rid[v - 2 * S] : v >= S ? eid[v - S] : id[v]; };
-  for (int b = 0; b < 256; ++b) {
-    put(4 * b, 4 * K * h.byte_class[b]);
-    put(1024 + 4 * b, 4 * h.byte_class[b]);
-  }
-  for (uint64_t x = 0; x < K2; ++x) {
-    put(pa + 4 * x, 4 * P * pc[x]);
-    put(pb + 4 * x, 4 * pc[x]);
-  }
-  for (uint64_t x = 0; x < K2; ++x)
-    for (uint64_t z = 0; z < K2; ++z) put(wc + 4 * (uint64_t(pc[x]) * P + pc[z]), 4 * wq[x * K2 + z]);
-  for (uint32_t i = 0; i < Sp; ++i) {
-    for (uint32_t w = 0; w < W; ++w) put(tw + uint64_t(i) * row + 4 * w, premul(code_id(F[size_t(wrep[w]) * S + orig[i]])));
-    for (uint32_t c = 0; c < K; ++c) put(t1 + 4 * (uint64_t(i) * K + c), premul(id[T(orig[i], c)]));
-  }
-  *start = premul(id[h.start]);
-  *start_m = premul(id[M]);
-  wa->pb = pb;
-  wa->wc = wc;
-  wa->tw = tw;
-  wa->t1 = uint32_t(t1);
-  wa->row = row;
-  wa->thr_e = premul(first_e);
-  wa->thr_r = premul(first_r);
-  wa->W = W;
-  wa->P = P;
-  *orig_out = orig;  // word state index -> blob state (a shadow -> the state it copies)
   return true;
 }
 
@@ -674,8 +522,8 @@ extern "C" void dgrep_close(dgrep_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_table, c->d_wide, c->d_full, c->d_ximg, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
-                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_seg_from, c->d_seg_state, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_order, c->d_counters,
+  void* bufs[] = {c->d_table, c->d_full, c->d_ximg, c->d_nfa, c->d_cls, c->d_spill, c->d_tails, c->d_chunk_nl, c->d_chunk_map,
+                  c->d_pend, c->d_long_tbl, c->d_st2id, c->d_seg, c->d_seg_off, c->d_segmap, c->d_seg_from, c->d_seg_state, c->d_tiles, c->d_out_off, c->d_line_base, c->d_staging, c->d_counters,
                   c->d_overflow, c->d_data, c->d_res_line, c->d_res_start, c->d_res_len, c->d_enc_scratch,
                   c->d_fname, c->d_bounds, c->d_enc_out, c->d_red_scratch, c->d_red_out};
   for (void* b : bufs)
@@ -720,10 +568,11 @@ extern "C" int dgrep_set_lane_chunk(dgrep_ctx* c, uint32_t chunk_bytes) {
   return DGREP_OK;
 }
 
-extern "C" int dgrep_set_stepper(dgrep_ctx* c, int force, uint32_t wide_hot_rows) {
-  if (!c || force < 0 || force > 5) return DGREP_E_INVALID;
+extern "C" int dgrep_set_stepper(dgrep_ctx* c, int force, uint32_t filter_rows) {
+  // 1 (the r01 wide stepper) and 5 (the r05 word stepper) were removed in round 6
+  if (!c || force < 0 || force > 4 || force == 1) return DGREP_E_INVALID;
   c->force_stepper = force;
-  c->wide_hot_rows_cap = wide_hot_rows ? wide_hot_rows : UINT32_MAX;
+  c->filter_rows_cap = filter_rows ? filter_rows : UINT32_MAX;
   return DGREP_OK;
 }
 
@@ -745,7 +594,6 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     }
   // expand byte classes into the kernel's LDS image
   std::vector<uint8_t> t;
-  std::vector<uint16_t> wide;
   uint32_t start = h.start, start_m = h.start_m;
   const int force = c->force_stepper;
   // a partial DFA (DGREP_DFA_PARTIAL) runs only as a filter: its last state is
@@ -758,15 +606,8 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   std::vector<uint8_t> pair_img;
   uint32_t pair_start = 0, pair_m = 0;
   std::vector<uint32_t> st2id;  // stepper state index -> blob state (long lines, see resolve_long_lines)
-  // the word stepper first (one lookup per 4 bytes), then the pair stepper
-  const bool want_word = !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_WORD_ENABLE) || force == 5);
-  const bool word_ok = want_word && build_word_image(h, trans, &pair_img, &pair_start, &pair_m, &c->word_args, &st2id);
-  if (force == 5 && !word_ok) {
-    c->err = "dgrep_load_dfa: the word stepper's tables do not fit this DFA";
-    return DGREP_E_UNSUPPORTED;
-  }
   const bool want_pair =
-      !partial && !word_ok && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3);
+      !partial && ((force == 0 && h.nstates > DGREP_SHENG_MAX_STATES && DGREP_PAIR_ENABLE) || force == 3);
   const bool pair_ok = want_pair && build_pair_image(h, trans, &pair_img, &pair_start, &pair_m, &c->pair_args, &st2id);
   if (force == 3 && !pair_ok) {
     c->err = "dgrep_load_dfa: the pair stepper's two-byte table does not fit this DFA";
@@ -774,15 +615,15 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   }
   std::vector<uint8_t> filter_img;
   uint32_t f_start = 0, f_m = 0, f_cend = UINT32_MAX;
-  const bool filter_ok = !pair_ok && !word_ok && ((force == 0 && (h.nstates > 256 || partial)) || force == 4) &&
-                         build_filter_image(h, trans, c->wide_hot_rows_cap, &filter_img, &f_start, &f_m, &f_cend,
+  const bool filter_ok = !pair_ok && ((force == 0 && (h.nstates > 256 || partial)) || force == 4) &&
+                         build_filter_image(h, trans, c->filter_rows_cap, &filter_img, &f_start, &f_m, &f_cend,
                                             partial ? h.nstates - 1 : UINT32_MAX);
   if ((force == 4 || partial) && !filter_ok) {
     c->err = "dgrep_load_dfa: the filter stepper cannot hold this DFA's first states";
     return DGREP_E_UNSUPPORTED;
   }
-  if (word_ok || pair_ok) {
-    c->step_kind = word_ok ? kStepWord : kStepPair;
+  if (pair_ok) {
+    c->step_kind = kStepPair;
     c->nclasses = h.nclasses;
     t.swap(pair_img);
     start = pair_start;
@@ -803,7 +644,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   if (c->d_ximg) HIPCHK(hipFree(c->d_ximg));
   c->d_ximg = nullptr;
   c->ximg_bytes = c->x_hot = c->x_rec = c->xr_off = 0;
-  if (pair_ok || word_ok) {
+  if (pair_ok) {
     // image built above
   } else if (filter_ok && partial) {
     const uint32_t* prog = trans + size_t(h.nstates) * h.nclasses;
@@ -864,37 +705,11 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
         if (k != cn && trans[size_t(x) * K + k] != x) absorbing = false;
       if (absorbing) c->blob_matched = bid[x];
     }
-  } else if (h.nstates > 256 || force == 1) {
-    if (h.nstates > 65535) {
-      c->err = "dgrep_load_dfa: DFA has " + std::to_string(h.nstates) +
-               " states; the wide stepper indexes states with u16 (at most 65535)";
-      return DGREP_E_UNSUPPORTED;
-    }
-    // StepWide: renumber hottest-first -- start, start_m, then breadth-first
-    // from start -- so the shallow states sit in the LDS-resident rows
-    c->step_kind = kStepWide;
-    const uint32_t S = h.nstates, K = h.nclasses;
-    std::vector<uint32_t> order, id(S, UINT32_MAX);
-    order.reserve(S);
-    auto visit = [&](uint32_t x) {
-      if (id[x] == UINT32_MAX) { id[x] = uint32_t(order.size()); order.push_back(x); }
-    };
-    visit(h.start);
-    visit(h.start_m);
-    for (size_t q = 0; q < order.size(); ++q)
-      for (uint32_t k = 0; k < K; ++k) visit(trans[size_t(order[q]) * K + k]);
-    for (uint32_t x = 0; x < S; ++x) visit(x);  // unreachable states (none in a minimal DFA)
-    wide.resize(size_t(S) * K);
-    for (uint32_t n = 0; n < S; ++n)
-      for (uint32_t k = 0; k < K; ++k) wide[size_t(n) * K + k] = uint16_t(id[trans[size_t(order[n]) * K + k]]);
-    start = id[h.start];
-    start_m = id[h.start_m];
-    const uint32_t hot_rows = std::min<uint32_t>({S, kWideHotBytes / (2 * K), c->wide_hot_rows_cap});
-    c->hot_entries = hot_rows * K;
-    c->nclasses = K;
-    t.assign((kWideClassBytes + size_t(c->hot_entries) * 2 + 15) & ~size_t(15), 0);
-    memcpy(t.data(), h.byte_class, 256);
-    memcpy(t.data() + kWideClassBytes, wide.data(), size_t(c->hot_entries) * 2);
+  } else if (h.nstates > 256) {
+    // the filter holds any DFA's first states (build_filter_image): only its
+    // forced row cap (dgrep_set_stepper) can leave a large DFA here
+    c->err = "dgrep_load_dfa: a DFA of " + std::to_string(h.nstates) + " states needs the filter stepper";
+    return DGREP_E_UNSUPPORTED;
   } else if (h.nstates <= DGREP_SHENG_MAX_STATES && force != 2) {
     // StepSheng8: V[b] = 8 bytes, byte s = next state of s on input byte b
     c->step_kind = kStepSheng8;
@@ -933,15 +748,9 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   }
   if (c->d_table) HIPCHK(hipFree(c->d_table));
   c->d_table = nullptr;
-  if (c->d_wide) HIPCHK(hipFree(c->d_wide));
-  c->d_wide = nullptr;
   c->table_bytes = uint32_t(t.size());
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_table), (t.size() + 15) & ~size_t(15)));
   HIPCHK(hipMemcpy(c->d_table, t.data(), t.size(), hipMemcpyHostToDevice));
-  if (!wide.empty()) {
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_wide), wide.size() * 2));
-    HIPCHK(hipMemcpy(c->d_wide, wide.data(), wide.size() * 2, hipMemcpyHostToDevice));
-  }
   c->flags = h.flags;
   c->nstates = h.nstates;
   c->start = start;
@@ -952,8 +761,7 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
   c->d_long_tbl = nullptr;
   c->d_st2id = nullptr;
   c->long_states = 0;
-  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepTable ||
-       c->step_kind == kStepWord) &&
+  if ((c->step_kind == kStepSheng8 || c->step_kind == kStepPair || c->step_kind == kStepTable) &&
       h.nstates <= 256 &&
       !st2id.empty()) {
     std::vector<uint8_t> lt(size_t(h.nstates) * 256);
@@ -1198,16 +1006,7 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   a.tails = c->d_tails;
   a.chunk_nl = park && !park_maps ? c->d_chunk_nl : nullptr;
   a.chunk_map = park_maps ? c->d_chunk_map : nullptr;
-  a.wide = c->d_wide;
   a.nclasses = c->nclasses;
-  a.hot_entries = c->hot_entries;
-  a.wd_pb = c->word_args.pb;
-  a.wd_wc = c->word_args.wc;
-  a.wd_tw = c->word_args.tw;
-  a.wd_t1 = c->word_args.t1;
-  a.wd_row = c->word_args.row;
-  a.wd_thr_e = c->word_args.thr_e;
-  a.wd_thr_r = c->word_args.thr_r;
   a.pair_t1 = c->pair_args.t1;
   a.pair_thr = c->pair_args.thr;
   a.pair_div = c->pair_args.div;
@@ -1230,26 +1029,6 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   // Anything else shows in the counters, and the ordering is queued again once
   // the extra passes have run.
   const bool speculate = !filt && capacity != 0;
-  // in-scan ordering: the per-tile aggregate / prefix entries (zeroed once)
-  const bool in_scan = speculate && DGREP_SCAN_ORDER;
-  if (in_scan && c->order_cap < ntiles) {
-    if (c->d_order) HIPCHK(hipFree(c->d_order));
-    c->d_order = nullptr;
-    c->order_cap = 0;
-    const uint64_t cap = ntiles + ntiles / 8 + 64;
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&c->d_order), 3 * cap * sizeof(uint64_t)));
-    HIPCHK(hipMemsetAsync(c->d_order, 0, 3 * cap * sizeof(uint64_t), c->stream));
-    c->order_cap = cap;
-  }
-  if (in_scan) {
-    a.out_line = d_line;
-    a.out_start = d_start;
-    a.out_len = d_len;
-    a.out_cap = capacity;
-    a.agg = c->d_order;
-    a.incl_c = c->d_order + c->order_cap;
-    a.incl_l = c->d_order + 2 * c->order_cap;
-  }
   // Each buffer a scan can outgrow (overflow list, pending list, the filter's
   // staging) is grown to what the scan counted and the scan re-run, so every
   // grow is followed by a scan that fits: at most three grows, four scans. (A
@@ -1263,26 +1042,24 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
     a.overflow_cap = c->overflow_cap;
     a.pend = park ? c->d_pend : nullptr;
     a.pend_cap = park ? c->pend_cap : 0;
-    // a fresh epoch per launch (16 bits, never 0): the previous launch's
-    // ordering entries read as not yet published
-    c->epoch = c->epoch % 0xffffu + 1u;
-    a.epoch = c->epoch;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, kCounters * sizeof(unsigned long long), c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     HIPCHK(scan_dfa(launch_kind(c), a, grid, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
-    if (speculate && !in_scan)
+    if (speculate)
       HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
                          d_line, d_start, d_len, c->stream));
     HIPCHK(hipMemcpyAsync(ctr, c->d_counters, sizeof ctr, hipMemcpyDeviceToHost, c->stream));
-    if (DGREP_SYNC_SPIN) {
+    if (DGREP_SYNC_SPIN_US > 0) {
       // block until the scan kernel is done (its wake-up latency overlaps the
-      // ordering passes), then poll the short tail (ordering, the 32-B count
-      // copy): the blocking wait alone returned tens of µs after the copy
+      // ordering passes), then poll the short tail, bounded (see DGREP_SYNC_SPIN_US)
       HIPCHK(hipEventSynchronize(c->ev1));
+      const auto t0 = std::chrono::steady_clock::now();
       hipError_t q;
-      while ((q = hipStreamQuery(c->stream)) == hipErrorNotReady) {
+      while ((q = hipStreamQuery(c->stream)) == hipErrorNotReady &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(DGREP_SYNC_SPIN_US)) {
       }
+      if (q == hipErrorNotReady) q = hipStreamSynchronize(c->stream);
       HIPCHK(q);
     } else {
       HIPCHK(hipStreamSynchronize(c->stream));
@@ -1430,7 +1207,6 @@ static int scan_resident(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, uint64
   // the speculative ordering stands unless the overflow pass, the long-line
   // resolution or the verification changed the staged lines since
   const bool order = total != 0 && total <= capacity && (!speculate || over || verify) && !ordered;
-  S.order_in_scan = in_scan && !order && !ordered ? 1u : 0u;
   if (order)
     HIPCHK(order_lines(c->d_tiles, c->d_staging, ntiles, c->d_out_off, c->d_line_base, c->staging_cap, capacity,
                        d_line, d_start, d_len, c->stream));
@@ -1780,9 +1556,12 @@ extern "C" int dgrep_take_kernel_ms(dgrep_ctx* c, double* sum_ms, uint64_t* scan
   return DGREP_OK;
 }
 
-extern "C" int dgrep_last_scan_stats(dgrep_ctx* c, dgrep_scan_stats* out) {
-  if (!c || !out) return DGREP_E_INVALID;
-  *out = c->stats;
+extern "C" int dgrep_last_scan_stats(dgrep_ctx* c, dgrep_scan_stats* out, size_t out_size) {
+  if (!c || !out || out_size == 0) return DGREP_E_INVALID;
+  // a shorter (older) caller layout gets its own size; a longer one a zeroed tail
+  const size_t k = std::min(out_size, sizeof(dgrep_scan_stats));
+  memcpy(out, &c->stats, k);
+  if (out_size > k) memset(reinterpret_cast<uint8_t*>(out) + k, 0, out_size - k);
   return DGREP_OK;
 }
 

@@ -60,7 +60,7 @@ EXPORTS = (
 )
 COMM_ID_BYTES = 128
 
-STEPPERS = {0: "table", 1: "sheng", 2: "wide", 3: "pair", 4: "filter", 5: "word"}
+STEPPERS = {0: "table", 1: "sheng", 3: "pair", 4: "filter"}
 
 KeyValue = namedtuple("KeyValue", ["Key", "Value"])  # map_reduce/helper_types.go:8-11
 
@@ -94,7 +94,7 @@ class _ScanStats(ctypes.Structure):
                 ("scan_attempts", ctypes.c_uint32), ("tiles", ctypes.c_uint64), ("overflow_lanes", ctypes.c_uint64),
                 ("matches", ctypes.c_uint64), ("scan_ms", ctypes.c_float), ("overflow_ms", ctypes.c_float),
                 ("verify_ms", ctypes.c_float), ("candidates", ctypes.c_uint64), ("pending", ctypes.c_uint64),
-                ("order_in_scan", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class _Gathered(ctypes.Structure):
@@ -180,7 +180,7 @@ def lib() -> ctypes.CDLL:
             L.dgrep_reduce.restype = i
             L.dgrep_reduce_free.argtypes = [ctypes.POINTER(_ReduceOut)]
             L.dgrep_reduce_free.restype = None
-            L.dgrep_last_scan_stats.argtypes = [vp, ctypes.POINTER(_ScanStats)]
+            L.dgrep_last_scan_stats.argtypes = [vp, ctypes.POINTER(_ScanStats), sz]
             L.dgrep_last_scan_stats.restype = i
             L.dgrep_build_info.argtypes = []
             L.dgrep_build_info.restype = ctypes.c_char_p
@@ -299,19 +299,18 @@ class Context:
         self._check(self._L.dgrep_set_stream(self._h, ctypes.c_void_p(hip_stream or None)))
 
     def set_lane_chunk(self, chunk_bytes: int = 0):
-        """Testing/tuning: the Sheng stepper's lane chunk for later scans
-        (dgrep_set_lane_chunk; 0 = adaptive)."""
+        """Testing/tuning: the Sheng / pair / filter lane chunk for later scans
+        (dgrep_set_lane_chunk; 0 = adaptive, else a multiple of 128 in [4096, 65536])."""
         self._check(self._L.dgrep_set_lane_chunk(self._h, chunk_bytes))
 
-    _FORCE = {"auto": 0, "wide": 1, "table": 2, "pair": 3, "filter": 4, "word": 5}
+    _FORCE = {"auto": 0, "table": 2, "pair": 3, "filter": 4}
 
-    def set_stepper(self, force=False, wide_hot_rows: int = 0):
+    def set_stepper(self, force="auto", filter_rows: int = 0):
         """Testing/tuning: the stepper the next load() uses (dgrep_set_stepper):
-        "auto" (default: by DFA size), "wide", "table" (u8, <= 256 states) or
-        "pair" (fails at load if its two-byte table does not fit), "filter"; True/False
-        mean "wide"/"auto". wide_hot_rows caps the wide stepper's LDS rows."""
-        mode = self._FORCE[force] if isinstance(force, str) else int(bool(force))
-        self._check(self._L.dgrep_set_stepper(self._h, mode, wide_hot_rows))
+        "auto" (default: by DFA size), "table" (u8, <= 256 states), "pair" (fails
+        at load if its two-byte table does not fit) or "filter"; filter_rows caps
+        the filter's LDS rows (nearly every line then becomes a candidate)."""
+        self._check(self._L.dgrep_set_stepper(self._h, self._FORCE[force], filter_rows))
 
     def load(self, pattern) -> CompiledPattern:
         cp = pattern if isinstance(pattern, CompiledPattern) else CompiledPattern(pattern)
@@ -418,7 +417,7 @@ class Context:
     def scan_stats(self) -> dict:
         """dgrep_last_scan_stats of the last scan (stepper, lane chunk, overflow lanes, times)."""
         st = _ScanStats()
-        self._check(self._L.dgrep_last_scan_stats(self._h, ctypes.byref(st)))
+        self._check(self._L.dgrep_last_scan_stats(self._h, ctypes.byref(st), ctypes.sizeof(st)))
         d = {f: getattr(st, f) for f, _ in _ScanStats._fields_}
         d["stepper"] = STEPPERS.get(d["stepper"], d["stepper"])
         return d

@@ -116,20 +116,22 @@ int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
  * two-byte table fits in LDS; else <= 256 states the u8 table; else the
  * filter: the DFA's shallowest states in LDS, lines that leave them verified
  * on the whole DFA).
- * force: 0 = that default, 1 = wide (u16, LDS-hot + HBM) for any DFA, 2 = the
- * u8 table (<= 256 states), 3 = pair (dgrep_load_dfa fails with
- * DGREP_E_UNSUPPORTED if it does not fit), 4 = filter (the default above 256
- * states), 5 = word (one lookup per 4-byte word; the default for > 8-state DFAs
- * whose word tables fit; DGREP_E_UNSUPPORTED if they do not). wide_hot_rows != 0
- * caps the LDS-resident rows of the wide stepper
- * and of the filter (whose cut then sends nearly every line to verification). */
-int dgrep_set_stepper(dgrep_ctx* ctx, int force, uint32_t wide_hot_rows);
-/* Tests / tuning: lane chunk of the Sheng (<= 8-state) and pair steppers for
- * later scans. 0 (default) = adaptive: the compiled 4 KiB chunk, doubled (up
- * to 32 KiB) while every resident wave still gets a tile and the matching
- * lines the previous scan's density predicts fill at most a quarter of a lane's
- * LDS slots; otherwise a multiple of 128 in [4096, 32768] (LDS slots hold
- * 16-bit chunk offsets). No effect on the u8 table and wide steppers. */
+ * force: 0 = that default, 2 = the u8 table (<= 256 states), 3 = pair
+ * (dgrep_load_dfa fails with DGREP_E_UNSUPPORTED if it does not fit), 4 =
+ * filter (the default above 256 states). 1 and 5 (the wide and word steppers
+ * of earlier rounds, measured slower and removed) and anything outside 0-5 are
+ * DGREP_E_INVALID. filter_rows != 0 caps the filter's LDS-resident rows (its
+ * cut then sends nearly every line to verification). */
+int dgrep_set_stepper(dgrep_ctx* ctx, int force, uint32_t filter_rows);
+/* Tests / tuning: lane chunk of the Sheng (<= 8-state), pair and filter
+ * steppers for later scans. 0 (default) = adaptive: the compiled 4 KiB chunk,
+ * doubled while every resident wave still gets a tile and the matching lines
+ * the previous scan's density predicts fill at most a quarter of a lane's
+ * record capacity, up to 32 KiB (Sheng, filter) or 8 KiB (pair). Otherwise a
+ * multiple of 128 in [4096, 65536] (the LDS slots hold 16-bit chunk offsets;
+ * a line starting exactly at a 64 KiB chunk end is flagged separately);
+ * anything else is DGREP_E_INVALID and leaves the setting unchanged. No effect
+ * on the u8 table stepper (fixed 2 KiB chunks). */
 int dgrep_set_lane_chunk(dgrep_ctx* ctx, uint32_t chunk_bytes);
 
 /* Host bytes -> H2D -> scan -> D2H results. This is the call Map makes.
@@ -270,9 +272,8 @@ int dgrep_take_kernel_ms(dgrep_ctx* ctx, double* sum_ms, uint64_t* scans);
 
 /* What the last dgrep_scan* call did (tests, tuning, bench reports). */
 typedef struct {
-  uint32_t stepper;        /* 0 u8 table, 1 Sheng (<= 8 states), 2 wide u16 table, 3 pair (two bytes per lookup),
-                              4 filter (shallow DFA states in LDS + candidate verification), 5 word (four bytes
-                              per lookup) */
+  uint32_t stepper;        /* 0 u8 table, 1 Sheng (<= 8 states), 3 pair (two bytes per lookup), 4 filter
+                              (shallow DFA states in LDS + candidate verification) */
   uint32_t lane_chunk;     /* bytes per lane chunk */
   uint32_t lane_slots;     /* LDS slots per lane chunk for matching lines */
   uint32_t scan_attempts;  /* scan launches (2 if the overflow list had to grow) */
@@ -285,10 +286,15 @@ typedef struct {
                               of the parked long lines */
   uint64_t candidates;     /* filter stepper: candidate lines dropped by that re-run */
   uint64_t pending;        /* Sheng: long lines parked by the scan and resolved from chunk maps */
-  uint32_t order_in_scan;  /* 1: the scan kernel placed the lines itself (no ordering pass ran after it) */
+  uint32_t reserved0;      /* round 5's order_in_scan (the in-scan ordering was removed in round 6): 0 */
   uint32_t reserved;
 } dgrep_scan_stats;
-int dgrep_last_scan_stats(dgrep_ctx* ctx, dgrep_scan_stats* out);
+/* Sized getter: out_size is the caller's sizeof(dgrep_scan_stats). The library
+ * writes min(out_size, its own size) bytes, so a binding built against an
+ * older (shorter) layout never has bytes written past its struct; a larger
+ * caller struct gets its tail zeroed. out_size 0 is DGREP_E_INVALID. The
+ * layout above is the round-5 one (80 bytes); fields are only ever appended. */
+int dgrep_last_scan_stats(dgrep_ctx* ctx, dgrep_scan_stats* out, size_t out_size);
 
 /* Provenance of this library: "head=<git commit>[-dirty] arch=gfx950
  * hipflags=<tuning -D knobs>" (static string). */

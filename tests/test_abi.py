@@ -120,3 +120,69 @@ def test_synth_kind4_plants_keywords_in_long_lines():
     found = sum(1 for k in kws if k in low)
     assert found >= 3, found
     assert bool(((a4 == 10) | ((a4 >= 0x20) & (a4 < 0x7f))).all())
+
+
+def _cpu_ctx():
+    """A context from dgrep_open on a machine without a GPU: the call fails
+    (DGREP_E_HIP) but hands back the context so the caller can read the message;
+    the setters below touch only host state."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: the GPU suite covers the setters through real scans")
+    L = dgrep.lib()
+    h = ctypes.c_void_p()
+    assert L.dgrep_open(0, ctypes.byref(h)) == dgrep.DGREP_E_HIP
+    assert h.value
+    return L, h
+
+
+def test_set_lane_chunk_accepts_exactly_the_documented_range():
+    """include/dgrep.h: 0 (adaptive) or a multiple of 128 in [4096, 65536];
+    anything else is DGREP_E_INVALID."""
+    L, h = _cpu_ctx()
+    try:
+        ok = [0, 4096, 4224, 8192, 12416, 32768, 32896, 65408, 65536]
+        bad = [1, 127, 128, 4000, 4095, 4097, 4160, 8193, 65537, 65664, 131072, 1 << 20, 0xFFFFFFFF]
+        for v in ok:
+            assert L.dgrep_set_lane_chunk(h, v) == dgrep.DGREP_OK, v
+        for v in bad:
+            assert L.dgrep_set_lane_chunk(h, v) == dgrep.DGREP_E_INVALID, v
+        # every multiple of 128 in range, and every non-multiple near the ends
+        for v in range(4096, 65536 + 1, 128):
+            assert L.dgrep_set_lane_chunk(h, v) == dgrep.DGREP_OK, v
+        for v in list(range(3968, 4096)) + list(range(65537, 65700)):
+            assert L.dgrep_set_lane_chunk(h, v) == dgrep.DGREP_E_INVALID, v
+    finally:
+        L.dgrep_close(h)
+
+
+def test_set_stepper_rejects_removed_steppers():
+    """dgrep_set_stepper: 0 auto, 2 table, 3 pair, 4 filter; 1 (wide) and 5
+    (word) were removed in round 6 and are DGREP_E_INVALID, as is anything else."""
+    L, h = _cpu_ctx()
+    try:
+        for f in (0, 2, 3, 4):
+            assert L.dgrep_set_stepper(h, f, 0) == dgrep.DGREP_OK, f
+        for f in (-1, 1, 5, 6, 100):
+            assert L.dgrep_set_stepper(h, f, 0) == dgrep.DGREP_E_INVALID, f
+    finally:
+        L.dgrep_close(h)
+
+
+def test_scan_stats_sized_getter():
+    """dgrep_last_scan_stats(ctx, out, out_size) never writes past out_size (a
+    binding built against a shorter layout) and zeroes a longer caller's tail."""
+    L, h = _cpu_ctx()
+    try:
+        full = ctypes.sizeof(dgrep._ScanStats)
+        assert full == 80
+        buf = (ctypes.c_uint8 * (full + 32))(*([0xAB] * (full + 32)))
+        assert L.dgrep_last_scan_stats(h, ctypes.cast(buf, ctypes.POINTER(dgrep._ScanStats)), 8) == dgrep.DGREP_OK
+        assert list(buf[8:]) == [0xAB] * (full + 24)   # nothing past the 8 bytes asked for
+        assert L.dgrep_last_scan_stats(h, ctypes.cast(buf, ctypes.POINTER(dgrep._ScanStats)), full + 16) == dgrep.DGREP_OK
+        assert list(buf[full:full + 16]) == [0] * 16    # a longer caller struct: zeroed tail
+        assert list(buf[full + 16:]) == [0xAB] * 16
+        assert L.dgrep_last_scan_stats(h, ctypes.cast(buf, ctypes.POINTER(dgrep._ScanStats)), 0) == dgrep.DGREP_E_INVALID
+    finally:
+        L.dgrep_close(h)

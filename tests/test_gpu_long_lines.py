@@ -49,8 +49,7 @@ STEPPER_PATTERNS = [
     ("auto", b"error"),                                   # Sheng (<= 8 states)
     ("auto", b""),                                        # every line
     ("auto", b"^[a-j ]*error[a-j ]*$"),                   # pair stepper (the default above 8 states)
-    ("word", b"^[a-j ]*error[a-j ]*$"),                   # word stepper (forced)
-    ("word", b"(WARN|ERROR) [a-z_]+"),
+    ("pair", b"(WARN|ERROR) [a-z_]+"),                    # pair stepper, C3's event pattern
     ("table", b"error$"),                                 # u8 table, two chunks per lane
     ("auto", b"(?i)e[r]+or"),
 ]
@@ -161,7 +160,6 @@ def _dense_then_long(chunk, long_len, long_matches, dense=b"error", seed=3):
     ("auto", b"error", 4096),                      # Sheng (chunk maps: parked at C + 4 KiB)
     ("auto", b"error", 32768),
     ("auto", b"^[a-j ]*error[a-j ]*$", 4096),      # pair (parked at 2 C)
-    ("word", b"^[a-j ]*error[a-j ]*$", 4096),      # word (parked at 2 C)
     ("table", b"error$", 0),                       # u8 table, two 2 KiB chunks per lane
 ])
 @pytest.mark.parametrize("long_matches", [False, True])

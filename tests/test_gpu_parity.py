@@ -7,6 +7,7 @@ oracle finishes in seconds; full-size runs are covered by bench.py's
 size-independent checks.
 """
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -78,7 +79,7 @@ def test_edge_inputs(gpu_ctx, pattern):
 
 @pytest.mark.parametrize("pattern", PATTERNS)
 def test_random_small(gpu_ctx, pattern):
-    rnd = random.Random(hash(pattern) & 0xffff)
+    rnd = random.Random(zlib.crc32(pattern) & 0xffff)
     alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b"K", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\r", b"\xe2\x82\xac",
              b"\xe2\x82", b"\xff", b"\xc5\xbf", b"WARN", b"ERROR", b"error", b"2024-01", b"key "]
     for _ in range(20):
@@ -140,7 +141,7 @@ def test_lane_chunk_validation(gpu_ctx):
     gpu_ctx.set_lane_chunk(0)
 
 
-@pytest.mark.parametrize("stepper", ["auto", "pair", "filter", "word"])
+@pytest.mark.parametrize("stepper", ["auto", "pair", "filter"])
 @pytest.mark.parametrize("chunk", [32768, 65536])
 def test_lines_starting_at_chunk_end(gpu_ctx, stepper, chunk):
     """A lane's last owned line can start exactly AT its chunk end (the chunk's
@@ -399,18 +400,19 @@ def test_map_reduce_surface(gpu_ctx):
     assert dgrep.Map("f", "a\n") == []
 
 
-# ---- the wide stepper (u16 table, hot rows in LDS, the rest in HBM) ---------
+# ---- the filter stepper forced on small DFAs (few LDS rows: nearly every line a candidate)
 @pytest.fixture
-def wide_ctx(gpu_ctx):
+def few_rows_ctx(gpu_ctx):
     yield gpu_ctx
-    gpu_ctx.set_stepper(False, 0)
+    gpu_ctx.set_stepper("auto", 0)
 
 
-@pytest.mark.parametrize("hot_rows", [0, 2])  # 0: as many LDS rows as fit; 2: nearly every row from HBM
+@pytest.mark.parametrize("rows", [0, 4])  # 0: as many LDS rows as fit; 4: nearly every line verified
 @pytest.mark.parametrize("pattern", PATTERNS)
-def test_wide_stepper_forced(wide_ctx, pattern, hot_rows):
-    wide_ctx.set_stepper(True, hot_rows)
-    rnd = random.Random(hash(pattern) & 0xfff)
+def test_filter_stepper_forced(few_rows_ctx, pattern, rows):
+    few_rows_ctx.set_stepper("filter", rows)
+    wide_ctx = few_rows_ctx
+    rnd = random.Random(zlib.crc32(pattern) & 0xfff)
     alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\xe2\x82\xac", b"\xff",
              b"WARN", b"ERROR", b"error", b"2024-01", b"key "]
     for n in (0, 1, 100, 5000, 70000, 300000):
@@ -418,10 +420,11 @@ def test_wide_stepper_forced(wide_ctx, pattern, hot_rows):
         _check(wide_ctx, pattern, data)
 
 
-def test_wide_stepper_boundaries_and_overflow(wide_ctx):
+def test_filter_stepper_boundaries_and_overflow(few_rows_ctx):
     import dgrep
 
-    wide_ctx.set_stepper(True, 3)
+    wide_ctx = few_rows_ctx
+    wide_ctx.set_stepper("filter", 4)
     for size in (1023, 1024, 1025, 65535, 65536, 65537, 3 * 65536 + 17):
         data = bytearray(dgrep.synth_corpus_host(size, 11, 0))
         for edge in (1023, 1024, 65535, 65536):
@@ -462,7 +465,7 @@ def filter_ctx(gpu_ctx):
 @pytest.mark.parametrize("pattern", PATTERNS)
 def test_filter_stepper_forced(filter_ctx, pattern, rows):
     filter_ctx.set_stepper("filter", rows)
-    rnd = random.Random(hash(pattern) & 0xfff)
+    rnd = random.Random(zlib.crc32(pattern) & 0xfff)
     alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\xe2\x82\xac", b"\xff",
              b"WARN", b"ERROR", b"error", b"2024-01", b"key "]
     for n in (0, 1, 100, 5000, 70000, 300000):
@@ -588,28 +591,18 @@ PAIR_PATTERNS = [b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"(WARN|ERROR) [a-
                  b"[^a-z ]{3}", b"^$|error", b"x*$|WARN"]
 
 
-@pytest.fixture(params=["pair", "word"])
-def pair_ctx(gpu_ctx, request):
-    # the pair stepper (two bytes per lookup) and the word stepper (four), also
-    # for DFAs the default gives to Sheng (<= 8 states)
-    gpu_ctx.set_stepper(request.param)
-    gpu_ctx.test_mode = request.param
+@pytest.fixture
+def pair_ctx(gpu_ctx):
+    # the pair stepper (two bytes per lookup), also for DFAs the default gives
+    # to Sheng (<= 8 states)
+    gpu_ctx.set_stepper("pair")
+    gpu_ctx.test_mode = "pair"
     yield gpu_ctx
     gpu_ctx.set_stepper("auto")
 
 
 def _load_mode(ctx, pattern):
-    """ctx.load, skipping a pattern whose tables the forced stepper cannot hold
-    (the word stepper's word tables, for a few patterns: the default then picks
-    the pair stepper)."""
-    import dgrep
-
-    try:
-        return ctx.load(pattern)
-    except dgrep.UnsupportedPattern:
-        if getattr(ctx, "test_mode", "") == "word":
-            pytest.skip("word tables do not fit: %r" % pattern)
-        raise
+    return ctx.load(pattern)
 
 
 @pytest.mark.parametrize("pattern", PAIR_PATTERNS + [b"error", b"", b"^$", b"(?i)k", b"\\x{FFFD}"])
@@ -620,7 +613,7 @@ def test_pair_stepper_edges_and_random(pair_ctx, pattern):
                  b"\xff\xfe\n\xe2\x82\xac\n\xe2\x82\n", b"a" * 5000 + b"WARN ab" + b"b" * 5000 + b"\nerror"]:
         _check(gpu_ctx, cp, data)
         assert gpu_ctx.scan_stats()["stepper"] == gpu_ctx.test_mode, pattern
-    rnd = random.Random(hash(pattern) & 0xffff)
+    rnd = random.Random(zlib.crc32(pattern) & 0xffff)
     alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\n\n", b"\r",
              b"\xe2\x82\xac", b"\xff", b"WARN ab", b"ERROR x", b"error", b"2024-01-02", b"key "]
     for _ in range(12):
@@ -628,8 +621,11 @@ def test_pair_stepper_edges_and_random(pair_ctx, pattern):
         _check(gpu_ctx, cp, b"".join(rnd.choice(alpha) for _ in range(n // 3)))
 
 
-@pytest.mark.parametrize("chunk", [4096, 8192, 32768, 65536])
+@pytest.mark.parametrize("chunk", [4096, 4224, 8192, 12416, 32768, 65536])
 def test_pair_stepper_chunk_and_tile_edges(pair_ctx, chunk):
+    """Chunk and tile edges at forced lane chunks, including odd multiples of
+    the 128-B block (4224 = 33 blocks, 12416 = 97): the wave-uniform in-chunk
+    loop steps two blocks per iteration and must stop exactly at C."""
     import dgrep
 
     gpu_ctx = pair_ctx
@@ -670,11 +666,11 @@ def test_pair_stepper_dense_overflow(pair_ctx):
 
 @pytest.mark.parametrize("chunk", [4096, 32768])
 def test_pair_deferred_events_line_shapes(pair_ctx, chunk):
-    """The pair stepper's deferred events (run_block_defer): matching and
-    non-matching lines of every length 1..260 B in a rotating order, so every
-    128-B block position holds an event word, a previous '\\n' in the same
-    word / an earlier word / an earlier block, and blocks with several '\\n' in
-    one word next to events (the exact per-word fallback)."""
+    """The pair stepper's event path: matching and non-matching lines of
+    every length 1..260 B in a rotating order, so every 128-B block position
+    holds an event word, a previous '\\n' in the same word / an earlier word /
+    an earlier block, and blocks with several '\\n' in one word next to events
+    (the general per-word loop)."""
     gpu_ctx = pair_ctx
     rnd = random.Random(chunk)
     lines = []
@@ -697,7 +693,7 @@ def test_pair_deferred_events_line_shapes(pair_ctx, chunk):
         gpu_ctx.set_lane_chunk(0)
 
 
-@pytest.mark.parametrize("mode", ["table", "pair", "wide", "word"])
+@pytest.mark.parametrize("mode", ["table", "pair", "filter"])
 def test_forced_steppers_agree_on_c3(gpu_ctx, mode):
     """C3's regex through each stepper that can hold it (dgrep_set_stepper)."""
     import dgrep

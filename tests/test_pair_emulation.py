@@ -9,6 +9,7 @@ pair from offset 0, then compares the matching line numbers with the oracle's
 restatement of grep.go Map. The GPU parity tests check the C++ builder and the
 kernel; this pins the algorithm itself, CPU only."""
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -99,7 +100,7 @@ PATTERNS = [b"^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+", b"(WARN|ERROR) [a-z_]+"
 def test_pair_algorithm_matches_oracle(pattern):
     cp = dgrep.CompiledPattern(pattern)
     P = build_pair(cp)
-    rnd = random.Random(hash(pattern) & 0xffff)
+    rnd = random.Random(zlib.crc32(pattern) & 0xffff)
     alpha = [b"a", b"e", b"r", b"o", b"x", b"k", b"K", b" ", b"_", b"1", b"-", b"\n", b"\n", b"\n\n", b"\r",
              b"\xe2\x82\xac", b"\xe2\x82", b"\xff", b"\xc5\xbf", b"WARN ab", b"ERROR x", b"error", b"2024-01",
              b"key ", b"timeout while waiting for lock", b"alpha7"]

@@ -19,10 +19,16 @@ for spec in "$@"; do
   (
     # the runtime builds the LDS images, so it takes the same knobs
     # the scan kernels' build parts in parallel (see scan_dfa.hip), then the runtime
+    # PARTS (default all): the scan build parts this variant recompiles; the
+    # others are linked from the normal build
     pp=()
     for k in 0 1 2 3 4; do
-      $HIPCC $FLAGS $defs -DDGREP_SCAN_PART=$k -c "$P/csrc/kernels/scan_dfa.hip" -o "$P/build/scan_dfa_${name}_p$k.o" 2> "$P/build/variant_${name}_p$k.log" &
-      pp+=($!)
+      if [[ " ${PARTS:-0 1 2 3 4} " == *" $k "* ]]; then
+        $HIPCC $FLAGS $defs -DDGREP_SCAN_PART=$k -c "$P/csrc/kernels/scan_dfa.hip" -o "$P/build/scan_dfa_${name}_p$k.o" 2> "$P/build/variant_${name}_p$k.log" &
+        pp+=($!)
+      else
+        cp "$P/build/scan_dfa_p$k.o" "$P/build/scan_dfa_${name}_p$k.o"
+      fi
     done
     $HIPCC $FLAGS $defs -c "$P/csrc/runtime/dgrep_runtime.hip" -o "$P/build/dgrep_runtime_$name.o" 2> "$P/build/variant_$name.log"
     for q in "${pp[@]}"; do wait "$q"; done
