@@ -74,6 +74,15 @@ WORKLOADS = {
     "long_c4": dict(pattern=None, seed=4, kind=4, gib=16.0, verify_window=256 << 10,
                     desc="long lines + C4 keywords: 16 GiB split (seed 4) of 4 MiB-mean lines between pages of log "
                          "lines, (?i) alternation of 1,000 seeded keywords (filter stepper)"),
+    # config 4's keywords OR "an even number of k" over the same long lines: a
+    # DFA (13,354 states) whose state depends on the whole line so far (the k
+    # parity), so about half of a parked line's segment guesses (the state after
+    # a 256-byte lookback) fail and those segments are re-run from the true state
+    # (long_dfa_fix_kernel). (k[^z]*y, the other unbounded-memory example, never
+    # fails a guess on this corpus: it holds no 'z' and a 'k' every ~40 bytes.)
+    "long_c4p": dict(pattern=None, extra="|^([^k]*k[^k]*k)*[^k]*$", seed=4, kind=4, gib=16.0, verify_window=256 << 10,
+                     desc="long lines + C4 keywords | even number of k: 16 GiB split (seed 4) of 4 MiB-mean lines, the "
+                          "filter stepper on an automaton with unbounded memory (segment guesses fail)"),
     # a dense Sheng line (~60 % of lines match): the lane chunk adapts to the match density
     "dense": dict(pattern="e", seed=2, kind=0, gib=16.0,
                   desc="dense: 16 GiB split (seed 2), literal 'e' (most lines match)"),
@@ -86,7 +95,7 @@ def workload_pattern(wl):
     if wl["pattern"] is not None:
         return wl["pattern"]
     import dgrep
-    return "(?i)(" + "|".join(k.decode() for k in dgrep.synth_keywords(wl["seed"], 1000)) + ")"
+    return "(?i)(" + "|".join(k.decode() for k in dgrep.synth_keywords(wl["seed"], 1000)) + ")" + wl.get("extra", "")
 
 
 

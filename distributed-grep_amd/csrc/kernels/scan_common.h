@@ -151,7 +151,12 @@ struct LongArgs {
   const uint2* sheng_v;
 };
 
-// the filter stepper's parked lines on the whole DFA (long_dfa_* kernels)
+// the filter stepper's parked lines on the whole DFA (long_dfa_* kernels):
+// each segment is run from up to kLongGuesses distinct entry guesses, the
+// states its lookback leads to from kLongSeeds start states
+constexpr int kLongSeeds = 8;
+constexpr int kLongGuesses = 4;
+constexpr uint32_t kNoGuess = 0xffffffffu;
 struct LongDfaArgs {
   const uint8_t* data;
   const void* full;       // [nstates][nclasses] breadth-first ids: u16, or u32 above 65535 states
@@ -161,11 +166,13 @@ struct LongDfaArgs {
   const uint8_t* cls;     // [256] byte classes (HBM)
   uint32_t start, start_m;
   uint32_t matched;       // the absorbing accepting state (UINT32_MAX: none)
+  uint32_t dead;          // the absorbing rejecting state (UINT32_MAX: none)
+  uint32_t seed[kLongSeeds];  // lookback start states: start, then states spread over the ids
   const LongSeg* seg;     // segments of the parked lines, line by line
   const uint64_t* seg_from;  // [nseg] where each segment's lookback starts
   uint64_t nseg;
-  uint32_t* seg_guess;    // [nseg] state after the lookback (the guessed entry state)
-  uint32_t* seg_exit;     // [nseg] state after the segment from the guess
+  uint32_t* seg_guess;    // [kLongGuesses][nseg] distinct states after the lookback (kNoGuess: unused)
+  uint32_t* seg_exit;     // [kLongGuesses][nseg] state after the segment from each guess
   const uint64_t* seg_off;  // [npend + 1]
   PendingLine* pend;
   uint64_t npend;

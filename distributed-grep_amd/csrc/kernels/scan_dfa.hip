@@ -732,13 +732,13 @@ __device__ __forceinline__ bool word_any(const Step& st, uint32_t M, uint32_t s0
 // the previous '\n' (an earlier word of the block, or r.prev_nl), all positions
 // are chunk-relative 32-bit values. Anything else (several '\n' in one word,
 // the part past the chunk end) takes the general loop.
-template <int J, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void word_emit_loop(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
-                                               uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
+template <class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_emit_loop(const Step& st, uint32_t M, uint32_t J, uint32_t m, uint32_t s0,
+                                               uint32_t s1, uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
                                                const Emitter<E, DIRECT>& emit);
-template <int J, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
-                                          uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
+template <class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t J, uint32_t m, uint32_t s0,
+                                          uint32_t s1, uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
                                           const Emitter<E, DIRECT>& emit) {
   if (!b.past && (m & (m - 1u)) == 0u) {
     // branch-free operands (selects, no nested exec-mask regions)
@@ -761,13 +761,13 @@ __device__ __forceinline__ void word_emit(const Step& st, uint32_t M, uint32_t m
       emit.inner(r, uint32_t(b.pos) + 4u * J + k, start, b.nlrun, cand_of(st, sk));
     return;
   }
-  word_emit_loop<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+  word_emit_loop(st, M, J, m, s0, s1, s2, s3, b, r, emit);
 }
 
 // word_emit's general loop: several '\n' in the word, or past the chunk end
-template <int J, class Step, int E, bool DIRECT>
-__device__ __forceinline__ void word_emit_loop(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
-                                               uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
+template <class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_emit_loop(const Step& st, uint32_t M, uint32_t J, uint32_t m, uint32_t s0,
+                                               uint32_t s1, uint32_t s2, uint32_t s3, const Blk& b, LaneRun& r,
                                                const Emitter<E, DIRECT>& emit) {
   const uint64_t q0 = b.pos + 4u * J;
   const bool nl_w = b.lnl >= kLnlBase;  // a '\n' in an earlier word of this block
@@ -834,12 +834,77 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
   const bool ev = word_any(st, M, s0, s1, s2, s3);
   if constexpr (((DGREP_EV_BALLOT) >> Step::kKind) & 1) {
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
-      if (ev) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+      if (ev) word_emit(st, M, J, m, s0, s1, s2, s3, b, r, emit);
     }
   } else {
-    if (__builtin_expect(ev, 0)) word_emit<J>(st, M, m, s0, s1, s2, s3, b, r, emit);
+    if (__builtin_expect(ev, 0)) word_emit(st, M, J, m, s0, s1, s2, s3, b, r, emit);
   }
   word_nl<J>(m, b);
+}
+
+// Deferred events (pair stepper, in-chunk blocks; DGREP_DEFER_EVENTS). The
+// per-word event path ran for the whole wave whenever ANY of its 64 lanes
+// ended a matching line in the word -- 27 % of C3's words for 1.2 lanes each,
+// ~30 instructions a time, 14 % of the kernel (no-event probes, same box:
+// 0.667 -> 0.572 of HBM peak). Instead, an event word only CAPTURES what its
+// record needs in four registers per lane (the line-start encoding lnl and the
+// '\n' count before the word, its newline mask, the two pair states) and the
+// block's end emits every lane's captured line at once, one pass for the whole
+// wave. A lane's second event in one block first emits the pending capture
+// (records stay in line order): rare, as lines are >= 40 bytes in text.
+struct EvCap {
+  uint32_t a;  // lnl | (J + 1) << 26 (lnl < 2^21); 0: nothing captured
+  uint32_t n;  // '\n' of the chunk before word J (Blk::nlrun)
+  uint32_t m;  // word J's newline mask (nl_mask)
+  uint32_t s;  // s1 | s3 << 16 (premultiplied pair states < 64 KiB)
+};
+template <class Step, int E, bool DIRECT>
+__device__ __forceinline__ void emit_cap(const Step& st, uint32_t M, const EvCap& c, const Blk& b, LaneRun& r,
+                                         const Emitter<E, DIRECT>& emit) {
+  Blk w = b;
+  w.lnl = c.a & ((1u << 26) - 1u);
+  w.nlrun = c.n;
+  const uint32_t s1 = c.s & 0xffffu, s3 = c.s >> 16;
+  word_emit(st, M, (c.a >> 26) - 1u, c.m, s1, s1, s3, s3, w, r, emit);
+}
+template <int J, class Step, int E, bool DIRECT>
+__device__ __forceinline__ void word_events_defer(const Step& st, uint32_t M, uint32_t m, uint32_t s1,
+                                                  uint32_t s3, Blk& b, LaneRun& r, const Emitter<E, DIRECT>& emit,
+                                                  EvCap& c) {
+  const bool ev = st.any2(s1, s3);
+  const uint64_t em = __builtin_amdgcn_ballot_w64(ev);
+  if (__builtin_expect(em != 0, 0)) {
+    // lanes with an event and a capture pending from earlier in the block
+    if (__builtin_expect((em & __builtin_amdgcn_ballot_w64(c.a != 0u)) != 0, 0)) {
+      if (ev && c.a != 0u) emit_cap(st, M, c, b, r, emit);
+    }
+    if (ev) {
+      c.a = b.lnl | uint32_t(J + 1) << 26;
+      c.n = b.nlrun;
+      c.m = m;
+      c.s = s1 | s3 << 16;
+    }
+  }
+  word_nl<J>(m, b);
+}
+// the block's captured lines, by the whole wave
+template <class Step, int E, bool DIRECT>
+__device__ __forceinline__ void flush_caps(const Step& st, uint32_t M, const EvCap& c, const Blk& b, LaneRun& r,
+                                           const Emitter<E, DIRECT>& emit) {
+#ifdef DGREP_DEFER_PROBE
+  asm volatile("" ::"v"(c.a), "v"(c.n), "v"(c.m), "v"(c.s));  // timing probe: captures dropped (wrong output)
+  return;
+#endif
+  if (__builtin_amdgcn_ballot_w64(c.a != 0u) != 0) {
+    if (c.a != 0u) emit_cap(st, M, c, b, r, emit);
+  }
+}
+#ifndef DGREP_DEFER_EVENTS
+#define DGREP_DEFER_EVENTS 1
+#endif
+template <class Step, bool DIRECT>
+constexpr bool defer_events() {
+  return DGREP_DEFER_EVENTS && Step::kKind == kStepPair && !DIRECT;
 }
 
 template <bool SENT>
@@ -920,11 +985,12 @@ constexpr bool pipe_chain() {
   return ((DGREP_PIPE_KINDS) >> Step::kKind) & 1;
 }
 
-template <int BK, class Step, int E, bool DIRECT>
+template <int BK, bool DEFER, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void run_block_pipe(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                                uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
   blk_init<sentinel<Step>()>(b, pos, C, r);
+  EvCap cap{0u, 0u, 0u, 0u};  // DEFER: this block's captured event per lane
   constexpr int NW = BK / 4;
   uint32_t w[NW];
 #pragma unroll
@@ -952,7 +1018,10 @@ __device__ __forceinline__ void run_block_pipe(const Step& st, uint32_t M, const
       if ((J) + 2 < NW) pb = st.prep(w[(J) + 2 < NW ? (J) + 2 : 0]);                     \
     }                                                                                     \
     const uint32_t m = nl_mask(w[(J) < NW ? (J) : 0]);                                    \
-    word_events<J>(st, M, m, s0, s1, s2, s3, b, r, emit);                                 \
+    if constexpr (DEFER)                                                                  \
+      word_events_defer<J>(st, M, m, s1, s3, b, r, emit, cap);                            \
+    else                                                                                  \
+      word_events<J>(st, M, m, s0, s1, s2, s3, b, r, emit);                               \
     s = s3;                                                                               \
   }
   DG_WP(0) DG_WP(1) DG_WP(2) DG_WP(3) DG_WP(4) DG_WP(5) DG_WP(6) DG_WP(7)
@@ -960,14 +1029,16 @@ __device__ __forceinline__ void run_block_pipe(const Step& st, uint32_t M, const
   DG_WP(16) DG_WP(17) DG_WP(18) DG_WP(19) DG_WP(20) DG_WP(21) DG_WP(22) DG_WP(23)
   DG_WP(24) DG_WP(25) DG_WP(26) DG_WP(27) DG_WP(28) DG_WP(29) DG_WP(30) DG_WP(31)
 #undef DG_WP
+  if constexpr (DEFER) flush_caps(st, M, cap, b, r, emit);
   blk_finish(b, s, r);
 }
 
-template <int BK, bool MAP, class Step, int E, bool DIRECT>
+// DEFER: in-chunk blocks of the uniform loop (run_lane_from), see defer_events
+template <int BK, bool MAP, class Step, int E, bool DIRECT, bool DEFER = false>
 __device__ __forceinline__ void run_block(const Step& st, uint32_t M, const uint4 (&v)[BK / 16], uint64_t pos,
                                           uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   if constexpr (!MAP && pipe_chain<Step>() && (Step::kKind == kStepPair || Step::kKind == kStepFilter)) {
-    run_block_pipe<BK>(st, M, v, pos, C, r, emit);
+    run_block_pipe<BK, DEFER>(st, M, v, pos, C, r, emit);
     return;
   }
   Blk b;
@@ -1224,6 +1295,8 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
     run_block<BK, kMap>(st, M, V, pos, uint64_t(C), r, emit);                              \
   else                                                                                     \
     run_block<BK, false>(st, M, V, pos, uint64_t(C), r, emit);
+// in-chunk blocks of the wave-uniform loop: no map mode (pair only), events deferred
+#define DG_STEP_U(V) run_block<BK, false, Step, E, DIRECT, defer_events<Step, DIRECT>()>(st, M, V, pos, uint64_t(C), r, emit);
 #define DG_CHECK                                                                           \
   if constexpr (kMap && kLazyMapBytes != 0) {                                              \
     if (maps && pos == kLazyMapBytes) {                                                    \
@@ -1268,6 +1341,7 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
     run_tail(st, M, p, pos, avail, uint64_t(C), r, nl_chunk, snap, emit);                  \
     break;                                                                                 \
   }
+  static_assert(!(uniform_main<Step, DIRECT>() && kMap), "the uniform in-chunk loop has no chunk-map mode");
   if constexpr (uniform_main<Step, DIRECT>()) {
     // The blocks inside the chunk of a wave whose lanes all hold C + BK bytes:
     // no lane leaves before C, so this loop's trip count is wave-uniform --
@@ -1287,7 +1361,7 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
           }
         }
         load_block<BK>(B, p + pos + BK);
-        DG_STEP(A, B)
+        DG_STEP_U(A)
         pos += BK;
         if constexpr (kMap && kLazyMapBytes != 0) {
           if (maps && pos == kLazyMapBytes) {
@@ -1298,7 +1372,7 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
           }
         }
         load_block<BK>(A, p + pos + BK);
-        DG_STEP(B, A)
+        DG_STEP_U(B)
         pos += BK;
       }
     }
@@ -1314,6 +1388,7 @@ __device__ __forceinline__ uint32_t run_lane_from(const ScanArgs& a, const Step&
     pos += BK;
   }
 #undef DG_STEP
+#undef DG_STEP_U
 #undef DG_CHECK
   if (!snap) nl_chunk = r.nl;
   return nl_chunk;
@@ -1684,21 +1759,6 @@ struct FullDfa {
     const uint32_t i = __umul24(s, K) + c;
     if (i < hot_n) return uint32_t(hot[i]);
     return cold(s, c, i);
-  }
-  // two chains at once (long_dfa_seg_kernel): both resident-row reads issued
-  // unconditionally (clamped), the cold path entered only when a lane of the
-  // wave needs it
-  __device__ __forceinline__ void next2(uint32_t& sa, uint32_t ba, uint32_t& sb, uint32_t bb) const {
-    const uint32_t ca = cls[ba], cb = cls[bb];
-    const uint32_t ia = __umul24(sa, K) + ca, ib = __umul24(sb, K) + cb;
-    uint32_t na = uint32_t(hot[min(ia, hot_n - 1u)]), nb = uint32_t(hot[min(ib, hot_n - 1u)]);
-    const bool ka = ia >= hot_n, kb = ib >= hot_n;
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(ka || kb) != 0, 0)) {
-      if (ka) na = cold(sa, ca, ia);
-      if (kb) nb = cold(sb, cb, ib);
-    }
-    sa = na;
-    sb = nb;
   }
   // a state past the resident rows: XI, its record (straight-line: the default
   // row's entry read unconditionally, then the exceptions selected) -- no HBM
@@ -2283,85 +2343,11 @@ constexpr int kLongDfaThreads = 1024;
 constexpr uint32_t kLongDfaHotBytes = 120 * 1024;  // rows alone (u32 DFAs)
 constexpr uint32_t kLongDfaLdsBytes = 158 * 1024;  // rows + DfaXRec (u16 DFAs)
 
-template <typename E, bool XI>
-__global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg_kernel(LongDfaArgs la) {
-  __shared__ uint32_t cls[256];
-  __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLongDfaLdsBytes];
-  if (threadIdx.x < 256) cls[threadIdx.x] = la.cls[threadIdx.x];
-  E* const hot = reinterpret_cast<E*>(lbuf);
-  const uint32_t hot_n = XI ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
-  if constexpr (XI) {
-    for (uint32_t i = threadIdx.x * 16u; i < la.ximg_bytes; i += kLongDfaThreads * 16u)
-      *reinterpret_cast<uint4*>(lbuf + i) = *reinterpret_cast<const uint4*>(la.ximg + i);
-  } else {
-    const E* full = static_cast<const E*>(la.full);
-    for (uint32_t i = threadIdx.x; i < hot_n; i += kLongDfaThreads) hot[i] = full[i];
-  }
-  __syncthreads();
-  FullDfa<E, XI> d{hot, (const __attribute__((address_space(1))) E*)la.full, cls, la.nclasses, hot_n};
-  if constexpr (XI) {
-    d.xr = reinterpret_cast<const uint2*>(lbuf + la.xr_off);
-    d.xh = la.x_hot;
-  }
-  // two segments per lane (g and g + half), stepped byte by byte in lockstep:
-  // the chain is a dependent table read per byte, so two chains per lane
-  // overlap their latencies. Each runs [lookback start, end) from `start`
-  // and snapshots its state at the segment's begin (the guess). MATCHED is
-  // absorbing in the table, so no early stop is needed.
-  const uint64_t half = (la.nseg + 1) / 2;
-  for (uint64_t g = uint64_t(blockIdx.x) * kLongDfaThreads + threadIdx.x; g < half;
-       g += uint64_t(gridDim.x) * kLongDfaThreads) {
-    const uint64_t h = g + half;
-    const bool two = h < la.nseg;
-    const LongSeg A = la.seg[g];
-    const LongSeg B = two ? la.seg[h] : LongSeg{0, 0};
-    const uint64_t fa = la.seg_from[g], fb = two ? la.seg_from[h] : 0;
-    uint32_t sa = la.start, sb = la.start, ga = la.start, gb = la.start;
-    // 32-bit positions relative to each run's 16-aligned start; the next
-    // 16-byte piece of both runs is loaded while this one is stepped
-    const uint64_t ba0 = fa & ~uint64_t(15), bb0 = fb & ~uint64_t(15);
-    const uint32_t lo_a = uint32_t(fa - ba0), beg_a = uint32_t(A.begin - ba0), end_a = uint32_t(A.end - ba0);
-    const uint32_t lo_b = uint32_t(fb - bb0), beg_b = two ? uint32_t(B.begin - bb0) : 0u,
-                   end_b = two ? uint32_t(B.end - bb0) : 0u;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    uint4 na4 = end_a ? *reinterpret_cast<const uint4*>(la.data + ba0) : z;
-    uint4 nb4 = end_b ? *reinterpret_cast<const uint4*>(la.data + bb0) : z;
-    for (uint32_t q = 0; q < end_a || q < end_b; q += 16) {
-      const uint4 va = na4, vb = nb4;
-      na4 = q + 16 < end_a ? *reinterpret_cast<const uint4*>(la.data + ba0 + q + 16) : z;
-      nb4 = q + 16 < end_b ? *reinterpret_cast<const uint4*>(la.data + bb0 + q + 16) : z;
-      const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t p = q + uint32_t(j);
-        if (p == beg_a) ga = sa;
-        if (p == beg_b) gb = sb;
-        const uint32_t xa = (wa[j >> 2] >> (8 * (j & 3))) & 0xffu, xb = (wb[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        uint32_t na = sa, nb = sb;
-        d.next2(na, xa, nb, xb);
-        sa = (p >= lo_a && p < end_a) ? na : sa;
-        sb = (p >= lo_b && p < end_b) ? nb : sb;
-      }
-    }
-    if (A.begin == fa) ga = la.start;  // no lookback: the line's first segment
-    if (B.begin == fb) gb = la.start;
-    la.seg_guess[g] = ga;
-    la.seg_exit[g] = sa;
-    if (two) {
-      la.seg_guess[h] = gb;
-      la.seg_exit[h] = sb;
-    }
-  }
-}
-
 // One segment per lane, read in 64-byte blocks (four 16-B loads, the next
 // block in flight while this one is stepped). Two segments per lane in
 // 16-B pieces kept 2,048 read streams per CU live, more 128-B lines than L2
 // holds: each line came from HBM several times (long_c4 seg kernel 21 ms per
 // 16 GiB, 0.67 TB/s of segment bytes).
-#ifndef DGREP_SEG_ONE
-#define DGREP_SEG_ONE 1
-#endif
 // 16-B pieces per block (4: 64 B, half a line: eight pieces spill at 1024 threads)
 #ifndef DGREP_SEG_PIECES
 #define DGREP_SEG_PIECES 4
@@ -2452,11 +2438,39 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
        g += uint64_t(gridDim.x) * kLongDfaThreads) {
     const LongSeg A = la.seg[g];
     const uint64_t fa = la.seg_from[g];
-    // the guess: the state after the lookback [fa, begin) from start (none
-    // for a line's first segment)
-    const uint32_t guess = A.begin == fa ? la.start : run(fa, A.begin, la.start);
-    la.seg_guess[g] = guess;
-    la.seg_exit[g] = run(A.begin, A.end, guess);
+    // The guesses: the states the lookback [fa, begin) leads to from start and
+    // from the seeds (kLongSeeds chains in lockstep), distinct, absorbing ones
+    // left out (the fix kernel stops there); a line's first segment has exactly
+    // one entry state, start. A DFA that forgets its past within the lookback
+    // (config 4's keywords) gives one guess; one that keeps a finite memory of
+    // the whole line (the parity of some byte, "a k since the last z") gives
+    // one guess per memory class, and the entry state is nearly always among them.
+    uint32_t gs[kLongGuesses];
+    uint32_t ng = 1;
+    gs[0] = la.start;
+    if (A.begin != fa) {
+      uint32_t sd[kLongSeeds];
+#pragma unroll
+      for (int i = 0; i < kLongSeeds; ++i) sd[i] = la.seed[i];
+      for_line_bytes(la.data, fa, A.begin, [&](uint32_t b) {
+        const uint32_t ce = cls[b];
+#pragma unroll
+        for (int i = 0; i < kLongSeeds; ++i) sd[i] = step_c(sd[i], ce);
+        return true;
+      });
+      ng = 0;
+#pragma unroll
+      for (int i = 0; i < kLongSeeds; ++i) {
+        bool fresh = sd[i] != la.matched && sd[i] != la.dead && ng < uint32_t(kLongGuesses);
+#pragma unroll
+        for (int k = 0; k < kLongGuesses; ++k) fresh = fresh && !(uint32_t(k) < ng && gs[k] == sd[i]);
+        if (fresh) gs[ng++] = sd[i];
+      }
+    }
+    for (uint32_t k = 0; k < uint32_t(kLongGuesses); ++k) {
+      la.seg_guess[k * la.nseg + g] = k < ng ? gs[k] : kNoGuess;
+      la.seg_exit[k * la.nseg + g] = k < ng ? run(A.begin, A.end, gs[k]) : kNoGuess;
+    }
   }
 }
 
@@ -2472,9 +2486,16 @@ __global__ __launch_bounds__(256) void long_dfa_fix_kernel(LongDfaArgs la) {
   for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < la.npend; i += uint64_t(gridDim.x) * 256) {
     PendingLine P = la.pend[i];
     uint32_t s = la.start;
-    for (uint64_t g = la.seg_off[i]; g < la.seg_off[i + 1] && s != la.matched; ++g) {
-      if (la.seg_guess[g] == s) {
-        s = la.seg_exit[g];
+    // in order from the true state: a segment whose guesses hold one is taken
+    // whole; else it is re-run from the true state (exact for any DFA); an
+    // absorbing state ends the walk
+    for (uint64_t g = la.seg_off[i]; g < la.seg_off[i + 1] && s != la.matched && s != la.dead; ++g) {
+      uint32_t x = kNoGuess;
+#pragma unroll
+      for (int k = 0; k < kLongGuesses; ++k)
+        if (x == kNoGuess && la.seg_guess[uint64_t(k) * la.nseg + g] == s) x = la.seg_exit[uint64_t(k) * la.nseg + g];
+      if (x != kNoGuess) {
+        s = x;
       } else {
         const LongSeg sg = la.seg[g];
         s = d.run(la.data, sg.begin, sg.end, s, la.matched);
@@ -2861,12 +2882,13 @@ hipError_t long_lines_sheng(const LongArgs& la, hipStream_t stream) {
 }
 
 uint32_t long_lookback() { return kLongLookback; }
-uint32_t long_segs_per_lane() { return DGREP_SEG_ONE ? 1u : 2u; }
+uint32_t long_guesses() { return uint32_t(kLongGuesses); }
+uint32_t long_seeds() { return uint32_t(kLongSeeds); }
 uint32_t long_dfa_hot_bytes() { return kLongDfaHotBytes; }
 uint32_t long_dfa_lds_bytes() { return kLongDfaLdsBytes; }
 
 hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
-  if (la.nseg && DGREP_SEG_ONE) {
+  if (la.nseg) {
     uint64_t grid = (la.nseg + kLongDfaThreads - 1) / kLongDfaThreads;
     if (grid > 65536) grid = 65536;
     if (u32)
@@ -2875,15 +2897,6 @@ hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream) {
       hipLaunchKernelGGL((long_dfa_seg1_kernel<uint16_t, true>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
     else
       hipLaunchKernelGGL((long_dfa_seg1_kernel<uint16_t, false>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
-  } else if (la.nseg) {
-    uint64_t grid = ((la.nseg + 1) / 2 + kLongDfaThreads - 1) / kLongDfaThreads;
-    if (grid > 65536) grid = 65536;
-    if (u32)
-      hipLaunchKernelGGL((long_dfa_seg_kernel<uint32_t, false>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
-    else if (la.ximg)
-      hipLaunchKernelGGL((long_dfa_seg_kernel<uint16_t, true>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
-    else
-      hipLaunchKernelGGL((long_dfa_seg_kernel<uint16_t, false>), dim3(grid), dim3(kLongDfaThreads), 0, stream, la);
   }
   uint64_t grid = (la.npend + 255) / 256;
   if (grid > 4096) grid = 4096;

@@ -74,7 +74,8 @@ hipError_t long_lines_dfa(const LongDfaArgs& la, bool u32, hipStream_t stream);
 uint32_t long_lookback();
 uint32_t long_dfa_hot_bytes();
 uint32_t long_dfa_lds_bytes();
-uint32_t long_segs_per_lane();
+uint32_t long_guesses();
+uint32_t long_seeds();
 uint32_t verify_hot_bytes();
 }  // namespace dgrep
 
@@ -115,6 +116,8 @@ struct dgrep_ctx {
   uint8_t* d_cls = nullptr;    // [256]
   uint32_t blob_start = 0, blob_start_m = 0;  // start / start_m in d_full's (breadth-first) ids
   uint32_t blob_matched = UINT32_MAX;          // the absorbing accepting state in d_full's ids (none: UINT32_MAX)
+  uint32_t blob_dead = UINT32_MAX;             // the absorbing rejecting state (none: UINT32_MAX)
+  std::vector<uint32_t> long_seed;             // lookback start states of long_dfa_seg1_kernel (d_full's ids)
   uint32_t verify_hot = 0;                     // leading entries of d_full verify_kernel keeps in LDS
   uint8_t* d_ximg = nullptr;                   // the whole-DFA LDS image (build_ximg; u16 DFAs that fit)
   uint32_t ximg_bytes = 0, x_hot = 0, x_rec = 0, xr_off = 0;
@@ -159,7 +162,7 @@ struct dgrep_ctx {
   // filter stepper: parked lines on the whole DFA (long_dfa_* kernels)
   uint64_t* d_seg_from = nullptr;
   uint64_t seg_from_cap = 0;
-  uint32_t* d_seg_state = nullptr;  // [2][nseg]: guess, exit
+  uint32_t* d_seg_state = nullptr;  // [2][guesses][nseg]: guesses, exits
   uint64_t seg_state_cap = 0;
 
   // dgrep_scan (host data) buffers
@@ -696,14 +699,34 @@ extern "C" int dgrep_load_dfa(dgrep_ctx* c, const void* blob, size_t n) {
     HIPCHK(hipMemcpy(c->d_cls, h.byte_class, 256, hipMemcpyHostToDevice));
     c->blob_start = bid[h.start];
     c->blob_start_m = bid[h.start_m];
-    // the absorbing accepting state (MATCHED): verification stops there
-    c->blob_matched = UINT32_MAX;
+    // the absorbing states: MATCHED (every byte but '\n' loops, '\n' ->
+    // start_m; verification stops there) and DEAD (the same with '\n' ->
+    // start: a line there never matches)
+    c->blob_matched = c->blob_dead = UINT32_MAX;
     const uint32_t cn = h.byte_class[uint8_t('\n')];
-    for (uint32_t x = 0; x < S && c->blob_matched == UINT32_MAX; ++x) {
-      bool absorbing = trans[size_t(x) * K + cn] == h.start_m;
+    for (uint32_t x = 0; x < S; ++x) {
+      bool absorbing = true;
       for (uint32_t k = 0; k < K && absorbing; ++k)
         if (k != cn && trans[size_t(x) * K + k] != x) absorbing = false;
-      if (absorbing) c->blob_matched = bid[x];
+      if (!absorbing) continue;
+      if (trans[size_t(x) * K + cn] == h.start_m && c->blob_matched == UINT32_MAX) c->blob_matched = bid[x];
+      if (trans[size_t(x) * K + cn] == h.start && c->blob_dead == UINT32_MAX) c->blob_dead = bid[x];
+    }
+    // long lines' lookback seeds: start, then states spread over the first
+    // breadth-first ids -- the rows the seg kernel holds in LDS, so a seed's
+    // first steps do not take the cold path -- never an absorbing one: a DFA
+    // keeping a finite memory of the whole line (a parity, a flag) has seeds
+    // in each memory class with high probability, so a segment's guesses cover
+    // its true entry state (long_c4p: 4.7 -> 485 GB/s)
+    const uint32_t NS = long_seeds();
+    const uint32_t H = std::min<uint32_t>(S, std::max<uint32_t>(
+                                                 64, c->x_hot ? c->x_hot : long_dfa_hot_bytes() / (esz * K)));
+    c->long_seed.assign(NS, c->blob_start);
+    for (uint32_t i = 1; i < NS && H > 2; ++i) {
+      uint32_t x = uint32_t(uint64_t(i) * (H - 1) / NS);
+      for (uint32_t t = 0; t < S && (x == c->blob_matched || x == c->blob_dead || x == c->blob_start); ++t)
+        x = (x + 1) % S;
+      c->long_seed[i] = x;
     }
   } else if (h.nstates > 256) {
     // the filter holds any DFA's first states (build_filter_image): only its
@@ -857,12 +880,13 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   HIPCHK(hipStreamSynchronize(c->stream));
   uint64_t total = 0;
   for (const PendingLine& p : P) total += p.end - p.line_start;
-  // two segments per lane of ONE round of long_dfa_seg_kernel (one 1024-thread
-  // workgroup per CU): a second, partly filled round held half the CUs idle
-  // for a whole segment (long_c4: 384 workgroups over 256 CUs). Each line adds
-  // at most one partial segment, hence the npend in the divisor. >= 16 KiB.
-  const uint64_t lanes2 = uint64_t(c->num_cus) * 1024 * long_segs_per_lane();
-  const uint64_t div = npend < lanes2 / 2 ? lanes2 - npend : uint64_t(c->num_cus) * 1536 * long_segs_per_lane();
+  // one segment per lane of ONE round of long_dfa_seg1_kernel (one
+  // 1024-thread workgroup per CU): a second, partly filled round held half the
+  // CUs idle for a whole segment (long_c4: 384 workgroups over 256 CUs). Each
+  // line adds at most one partial segment, hence the npend in the divisor.
+  // >= 16 KiB.
+  const uint64_t lanes2 = uint64_t(c->num_cus) * 1024;
+  const uint64_t div = npend < lanes2 / 2 ? lanes2 - npend : uint64_t(c->num_cus) * 1536;
   const uint64_t seg = std::max<uint64_t>(uint64_t(16) << 10, (total / div + 16) & ~uint64_t(15));
   std::vector<LongSeg> segs;
   std::vector<uint64_t> from, off(npend + 1, 0);
@@ -877,7 +901,8 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   const uint64_t ns = std::max<uint64_t>(segs.size(), 1);
   if ((rc = grow(c, &c->d_seg, &c->seg_cap, ns)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_seg_from, &c->seg_from_cap, ns)) != DGREP_OK) return rc;
-  if ((rc = grow(c, &c->d_seg_state, &c->seg_state_cap, 2 * ns)) != DGREP_OK) return rc;
+  const uint64_t ng = long_guesses();
+  if ((rc = grow(c, &c->d_seg_state, &c->seg_state_cap, 2 * ng * ns)) != DGREP_OK) return rc;
   if ((rc = grow(c, &c->d_seg_off, &c->seg_off_cap, npend + 1)) != DGREP_OK) return rc;
   if (!segs.empty()) {
     HIPCHK(hipMemcpyAsync(c->d_seg, segs.data(), segs.size() * sizeof(LongSeg), hipMemcpyHostToDevice, c->stream));
@@ -898,11 +923,13 @@ static int resolve_long_filter(dgrep_ctx* c, const uint8_t* d_data, uint64_t n, 
   la.start = c->blob_start;
   la.start_m = c->blob_start_m;
   la.matched = c->blob_matched;
+  la.dead = c->blob_dead;
+  for (uint32_t i = 0; i < long_seeds() && i < uint32_t(kLongSeeds); ++i) la.seed[i] = c->long_seed[i];
   la.seg = c->d_seg;
   la.seg_from = c->d_seg_from;
   la.nseg = segs.size();
   la.seg_guess = c->d_seg_state;
-  la.seg_exit = c->d_seg_state + ns;
+  la.seg_exit = c->d_seg_state + ng * ns;
   la.seg_off = c->d_seg_off;
   la.pend = c->d_pend;
   la.npend = npend;

@@ -279,3 +279,40 @@ def test_filter_long_lines_large_keyword_dfa(gpu_ctx):
     data = b"\n".join(parts)
     st = _check(gpu_ctx, b"(?i)(" + b"|".join(kws) + b")", data)
     assert st["stepper"] == "filter" and st["pending"] > 0, st
+
+
+@pytest.mark.parametrize("extra", [b"|^([^k]*k[^k]*k)*[^k]*$",     # an even number of k (parity: never forgets)
+                                   b"|^([^k]*k[^k]*k[^k]*k)*[^k]*$",  # k count divisible by 3
+                                   b"|k[^z]*y"])                     # a k since the last z, then y
+def test_filter_long_lines_unbounded_memory(gpu_ctx, extra):
+    """Parked filter lines whose DFA keeps a finite memory of the WHOLE line
+    (config 4's keywords OR a k-parity / k-count-mod-3 / k-then-y branch):
+    a segment's entry state is not the state its 256-byte lookback reaches from
+    start, so the seg kernel's extra lookback seeds must supply the right guess
+    (or the fix kernel re-runs the segment from the true state). Lines of
+    0.3-3 MiB whose k count / z placement is chosen so that both verdicts
+    occur, the bench workload long_c4p's corpus (synth kind 4), bit-exact vs
+    the oracle."""
+    import dgrep
+
+    rnd = random.Random(zlib_crc(extra))
+    words = [b"request", b"user", b"cache", b"latency", b"retry", b"shard", b"value", b"node", b"kind", b"yes",
+             b"zone"]
+    parts = []
+    for i in range(10):
+        L = rnd.randrange(300 << 10, 3 << 20)
+        body = bytearray(b" ".join(rnd.choice(words) for _ in range(L // 5))[:L])
+        if i % 2:  # flip the k parity of the line at a random place
+            q = rnd.randrange(L)
+            body[q] = ord("k") if body[q] != ord("k") else ord("x")
+        parts.append(bytes(body))
+        parts.append(dgrep.synth_corpus_host(rnd.randrange(100, 20000), 700 + i, 1).rstrip(b"\n"))
+    data = b"\n".join(parts) + b"\n" + dgrep.synth_corpus_host(20 << 20, 4, 4)
+    st = _check(gpu_ctx, _c4_pattern() + extra, data)
+    assert st["stepper"] == "filter" and st["pending"] > 0, st
+
+
+def zlib_crc(b):
+    import zlib
+
+    return zlib.crc32(b)
