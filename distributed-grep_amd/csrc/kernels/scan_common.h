@@ -274,6 +274,12 @@ constexpr uint32_t kPairMaxT2 = 32768;
 constexpr int kKindW32 = 0x100;
 constexpr uint32_t kPairMaxImage = 40960;
 constexpr uint32_t kPairT2 = 2048;  // LDS address of T2 (after the byte tables)
+// DGREP_PAIR_CK: a second byte table CK[b] = esz K class(b) (u16 at kPairCK) for
+// the first byte of each pair, so a pair's column needs no v_mul_u32_u24
+#ifndef DGREP_PAIR_CK
+#define DGREP_PAIR_CK 1
+#endif
+constexpr uint32_t kPairCK = 256;
 // The filter's one workgroup per CU: 1024 threads (4 waves per SIMD) with
 // 128-byte load blocks. With 64-byte blocks it fetched 1.82x the split from
 // HBM (each lane's half-read 128-byte lines are evicted before their second

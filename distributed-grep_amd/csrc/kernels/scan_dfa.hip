@@ -267,6 +267,22 @@ struct StepPairT {
     uint32_t a0, a2;
   };
   __device__ __forceinline__ Pre prep(uint32_t x) const {
+    if constexpr (DGREP_PAIR_CK) {
+      // bytes 0 and 2 from the u16 table CK[b] = esz K class(b) at kPairCK, bytes
+      // 1 and 3 from C: a pair's column is CK[b0] + C[b1], no v_mul. The CK
+      // addresses 2 b as ONE v_lshlrev_b32_sdwa each (byte select in the shift)
+      uint32_t o0, o2;
+      asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+          : "=v"(o0)
+          : "v"(1u), "v"(x));
+      asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+          : "=v"(o2)
+          : "v"(1u), "v"(x));
+      uint32_t k0 = *reinterpret_cast<const uint16_t*>(lds + kPairCK + o0), c1 = lds[(x >> 8) & 0xffu],
+               k2 = *reinterpret_cast<const uint16_t*>(lds + kPairCK + o2), c3 = lds[x >> 24];
+      asm("" : "+v"(k0), "+v"(c1), "+v"(k2), "+v"(c3));
+      return Pre{k0 + c1, k2 + c3};
+    }
     uint32_t c0 = lds[x & 0xffu], c1 = lds[(x >> 8) & 0xffu], c2 = lds[(x >> 16) & 0xffu], c3 = lds[x >> 24];
     // pinned as 32-bit values: carried across a branch as i8 they are re-masked
     asm("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
@@ -853,7 +869,8 @@ __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t
 // wave. A lane's second event in one block first emits the pending capture
 // (records stay in line order): rare, as lines are >= 40 bytes in text.
 struct EvCap {
-  uint32_t a;  // lnl | (J + 1) << 26 (lnl < 2^21); 0: nothing captured
+  uint64_t lanes;  // wave-uniform: the lanes holding a capture
+  uint32_t a;  // lnl | (J + 1) << 26 (lnl < 2^21)
   uint32_t n;  // '\n' of the chunk before word J (Blk::nlrun)
   uint32_t m;  // word J's newline mask (nl_mask)
   uint32_t s;  // s1 | s3 << 16 (premultiplied pair states < 64 KiB)
@@ -875,9 +892,11 @@ __device__ __forceinline__ void word_events_defer(const Step& st, uint32_t M, ui
   const uint64_t em = __builtin_amdgcn_ballot_w64(ev);
   if (__builtin_expect(em != 0, 0)) {
     // lanes with an event and a capture pending from earlier in the block
-    if (__builtin_expect((em & __builtin_amdgcn_ballot_w64(c.a != 0u)) != 0, 0)) {
-      if (ev && c.a != 0u) emit_cap(st, M, c, b, r, emit);
+    const uint64_t fl = em & c.lanes;
+    if (__builtin_expect(fl != 0, 0)) {
+      if ((fl >> (threadIdx.x & 63u)) & 1u) emit_cap(st, M, c, b, r, emit);
     }
+    c.lanes |= em;
     if (ev) {
       c.a = b.lnl | uint32_t(J + 1) << 26;
       c.n = b.nlrun;
@@ -891,12 +910,8 @@ __device__ __forceinline__ void word_events_defer(const Step& st, uint32_t M, ui
 template <class Step, int E, bool DIRECT>
 __device__ __forceinline__ void flush_caps(const Step& st, uint32_t M, const EvCap& c, const Blk& b, LaneRun& r,
                                            const Emitter<E, DIRECT>& emit) {
-#ifdef DGREP_DEFER_PROBE
-  asm volatile("" ::"v"(c.a), "v"(c.n), "v"(c.m), "v"(c.s));  // timing probe: captures dropped (wrong output)
-  return;
-#endif
-  if (__builtin_amdgcn_ballot_w64(c.a != 0u) != 0) {
-    if (c.a != 0u) emit_cap(st, M, c, b, r, emit);
+  if (c.lanes != 0) {
+    if ((c.lanes >> (threadIdx.x & 63u)) & 1u) emit_cap(st, M, c, b, r, emit);
   }
 }
 #ifndef DGREP_DEFER_EVENTS
@@ -990,7 +1005,7 @@ __device__ __forceinline__ void run_block_pipe(const Step& st, uint32_t M, const
                                                uint64_t C, LaneRun& r, const Emitter<E, DIRECT>& emit) {
   Blk b;
   blk_init<sentinel<Step>()>(b, pos, C, r);
-  EvCap cap{0u, 0u, 0u, 0u};  // DEFER: this block's captured event per lane
+  EvCap cap{0ull, 0u, 0u, 0u, 0u};  // DEFER: this block's captured event per lane
   constexpr int NW = BK / 4;
   uint32_t w[NW];
 #pragma unroll
@@ -2334,6 +2349,7 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
 // state, takes a segment's exit when its guess was right and re-runs the
 // segment from the true state when it was not (exact for any DFA).
 constexpr uint32_t kLongLookback = 256;
+constexpr uint64_t kLongSeedBytes = 64;  // lookback bytes every seed steps (long_dfa_seg1_kernel)
 
 
 // one 1024-thread workgroup per CU holds the DFA's first kLongDfaHotBytes of
@@ -2445,6 +2461,10 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
     // (config 4's keywords) gives one guess; one that keeps a finite memory of
     // the whole line (the parity of some byte, "a k since the last z") gives
     // one guess per memory class, and the entry state is nearly always among them.
+    // The seeds run together over the lookback's first kLongSeedBytes only:
+    // chains that meet there stay together, so the rest of the lookback steps
+    // just the distinct ones (config 4's keyword automaton: one chain after ~12
+    // bytes; a parity: two).
     uint32_t gs[kLongGuesses];
     uint32_t ng = 1;
     gs[0] = la.start;
@@ -2452,7 +2472,8 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
       uint32_t sd[kLongSeeds];
 #pragma unroll
       for (int i = 0; i < kLongSeeds; ++i) sd[i] = la.seed[i];
-      for_line_bytes(la.data, fa, A.begin, [&](uint32_t b) {
+      const uint64_t mid = min(A.begin, fa + kLongSeedBytes);
+      for_line_bytes(la.data, fa, mid, [&](uint32_t b) {
         const uint32_t ce = cls[b];
 #pragma unroll
         for (int i = 0; i < kLongSeeds; ++i) sd[i] = step_c(sd[i], ce);
@@ -2466,6 +2487,8 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
         for (int k = 0; k < kLongGuesses; ++k) fresh = fresh && !(uint32_t(k) < ng && gs[k] == sd[i]);
         if (fresh) gs[ng++] = sd[i];
       }
+      if (ng == 0) gs[ng++] = sd[0];  // every seed absorbed: the fix kernel stops before this segment anyway
+      for (uint32_t k = 0; k < ng; ++k) gs[k] = run(mid, A.begin, gs[k]);
     }
     for (uint32_t k = 0; k < uint32_t(kLongGuesses); ++k) {
       la.seg_guess[k * la.nseg + g] = k < ng ? gs[k] : kNoGuess;

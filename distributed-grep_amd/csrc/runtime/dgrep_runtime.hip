@@ -390,9 +390,14 @@ bool build_pair_image(const dgrep_blob_header& h, const uint32_t* trans, std::ve
       }
     }
   }
-  // one u8 table C[b] = esz class(b) at LDS 0; esz (K - 1) < 256
+  // one u8 table C[b] = esz class(b) at LDS 0; esz (K - 1) < 256; and (for
+  // the pair's first byte) CK[b] = esz K class(b), u16 at kPairCK
   if (esz * (K - 1u) > 255u) return false;
-  for (int b = 0; b < 256; ++b) img->data()[b] = uint8_t(esz * h.byte_class[b]);
+  for (int b = 0; b < 256; ++b) {
+    img->data()[b] = uint8_t(esz * h.byte_class[b]);
+    const uint16_t ck = uint16_t(esz * K * h.byte_class[b]);
+    memcpy(img->data() + kPairCK + 2 * b, &ck, 2);
+  }
   *start = premul(id[h.start]);
   *start_m = premul(id[M]);
   *orig_out = orig;  // pair state index -> blob state (a shadow -> the state it copies)
