@@ -161,7 +161,7 @@ struct LongDfaArgs {
   const uint8_t* data;
   const void* full;       // [nstates][nclasses] breadth-first ids: u16, or u32 above 65535 states
   uint32_t hot_entries;   // leading entries of `full` in LDS (long_dfa_fix_kernel)
-  uint32_t seg_hot_entries;  // the same for long_dfa_seg_kernel (a larger LDS copy)
+  uint32_t seg_hot_entries;  // the same for long_dfa_seg1_kernel (a larger LDS copy)
   uint32_t nclasses;
   const uint8_t* cls;     // [256] byte classes (HBM)
   uint32_t start, start_m;

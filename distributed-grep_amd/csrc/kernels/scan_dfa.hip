@@ -55,7 +55,7 @@
 
 // Build parts: the Makefile compiles this file once per DGREP_SCAN_PART -- 0:
 // the kernels that take no stepper (verification, long lines, ordering) and
-// the host glue; 1: Sheng; 2: pair; 3: table; 4: filter + wide -- so the
+// the host glue; 1: Sheng; 2: pair; 3: table; 4: filter -- so the
 // stepper instantiations compile in parallel. Without the macro one
 // translation unit holds everything (tools/build_commit_variant.sh).
 #ifdef DGREP_SCAN_PART
@@ -2339,17 +2339,22 @@ __global__ __launch_bounds__(kLsThreads) void long_sheng_kernel(LongArgs la) {
 // ---- long lines of the filter stepper (> 256 states) ---------------------------
 // A parked line is decided on the WHOLE DFA (breadth-first ids, u16/u32 table in
 // HBM with its leading rows in LDS, as verify_kernel) in parallel over its
-// bytes: the host cuts [line_start, end) into segments; long_dfa_seg_kernel
-// runs each segment on one lane from a GUESSED entry state -- the state the
-// DFA reaches from `start` over the kLongLookback bytes before the segment
-// (for keyword automata such as config 4's, the state after any 12+ bytes no
-// longer depends on what came before, so the guess is exact) -- and records
-// guess, exit state and whether the absorbing MATCHED state was reached;
+// bytes: the host cuts [line_start, end) into segments; long_dfa_seg1_kernel
+// runs each segment on one lane from up to kLongGuesses GUESSED entry states --
+// the states the DFA reaches over the kLongLookback bytes before the segment
+// from kLongSeeds start states (for keyword automata such as config 4's, the
+// state after any 12+ bytes no longer depends on what came before, so one
+// guess is exact) -- and records each guess with its exit state;
 // long_dfa_fix_kernel then walks each line's segments in order from the true
 // state, takes a segment's exit when its guess was right and re-runs the
 // segment from the true state when it was not (exact for any DFA).
 constexpr uint32_t kLongLookback = 256;
 constexpr uint64_t kLongSeedBytes = 64;  // lookback bytes every seed steps (long_dfa_seg1_kernel)
+#ifndef DGREP_LONG_SEEDS_RUN
+#define DGREP_LONG_SEEDS_RUN kLongSeeds  // seeds stepped (<= kLongSeeds; 1: start only, the round-5 single guess)
+#endif
+constexpr int kLongSeedsRun = DGREP_LONG_SEEDS_RUN;
+static_assert(kLongSeedsRun >= 1 && kLongSeedsRun <= kLongSeeds, "DGREP_LONG_SEEDS_RUN");
 
 
 // one 1024-thread workgroup per CU holds the DFA's first kLongDfaHotBytes of
@@ -2369,12 +2374,26 @@ constexpr uint32_t kLongDfaLdsBytes = 158 * 1024;  // rows + DfaXRec (u16 DFAs)
 #define DGREP_SEG_PIECES 4
 #endif
 constexpr int kSegPieces = DGREP_SEG_PIECES;
+#ifndef DGREP_SEG_CLS8
+#define DGREP_SEG_CLS8 1
+#endif
 template <typename E, bool XI>
 __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaArgs la) {
   __shared__ uint32_t cls[256];
+  __shared__ uint8_t cls8[256];
   __shared__ __attribute__((aligned(16))) uint8_t lbuf[kLongDfaLdsBytes];
   // classes pre-scaled to the entry size: a step's table address is one v_mad
-  if (threadIdx.x < 256) cls[threadIdx.x] = uint32_t(la.cls[threadIdx.x]) * uint32_t(sizeof(E));
+  if (threadIdx.x < 256) {
+    cls[threadIdx.x] = uint32_t(la.cls[threadIdx.x]) * uint32_t(sizeof(E));
+    cls8[threadIdx.x] = uint8_t(la.cls[threadIdx.x]);
+  }
+  // a byte's scaled class. CLS8: from the u8 copy -- bytes b and b + 128 share
+  // a bank, so ASCII text reads it conflict-free (the u32 table's bank is b % 32:
+  // 'a', 'A' and '!' collide) -- for one more VALU op per byte
+  auto cl = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {
+    if constexpr (DGREP_SEG_CLS8) return uint32_t(cls8[b]) * uint32_t(sizeof(E));
+    return cls[b];
+  };
   E* const hot = reinterpret_cast<E*>(lbuf);
   const uint32_t hot_n = XI ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
   if constexpr (XI) {
@@ -2404,13 +2423,13 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
     return t;
   };
   auto step = [&](uint32_t s, uint32_t byte) __attribute__((always_inline)) -> uint32_t {
-    return step_c(s, cls[byte]);
+    return step_c(s, cl(byte));
   };
   auto word_cls = [&](uint32_t w, uint32_t (&c)[4]) __attribute__((always_inline)) {
-    c[0] = cls[w & 0xffu];
-    c[1] = cls[(w >> 8) & 0xffu];
-    c[2] = cls[(w >> 16) & 0xffu];
-    c[3] = cls[w >> 24];
+    c[0] = cl(w & 0xffu);
+    c[1] = cl((w >> 8) & 0xffu);
+    c[2] = cl((w >> 16) & 0xffu);
+    c[3] = cl(w >> 24);
   };
   // state after bytes [a, e) from s: the bytes up to the first 64-B boundary
   // and after the last one singly, the blocks between unrolled with no
@@ -2469,19 +2488,19 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
     uint32_t ng = 1;
     gs[0] = la.start;
     if (A.begin != fa) {
-      uint32_t sd[kLongSeeds];
+      uint32_t sd[kLongSeedsRun];
 #pragma unroll
-      for (int i = 0; i < kLongSeeds; ++i) sd[i] = la.seed[i];
+      for (int i = 0; i < kLongSeedsRun; ++i) sd[i] = la.seed[i];
       const uint64_t mid = min(A.begin, fa + kLongSeedBytes);
       for_line_bytes(la.data, fa, mid, [&](uint32_t b) {
-        const uint32_t ce = cls[b];
+        const uint32_t ce = cl(b);
 #pragma unroll
-        for (int i = 0; i < kLongSeeds; ++i) sd[i] = step_c(sd[i], ce);
+        for (int i = 0; i < kLongSeedsRun; ++i) sd[i] = step_c(sd[i], ce);
         return true;
       });
       ng = 0;
 #pragma unroll
-      for (int i = 0; i < kLongSeeds; ++i) {
+      for (int i = 0; i < kLongSeedsRun; ++i) {
         bool fresh = sd[i] != la.matched && sd[i] != la.dead && ng < uint32_t(kLongGuesses);
 #pragma unroll
         for (int k = 0; k < kLongGuesses; ++k) fresh = fresh && !(uint32_t(k) < ng && gs[k] == sd[i]);
@@ -2511,12 +2530,30 @@ __global__ __launch_bounds__(256) void long_dfa_fix_kernel(LongDfaArgs la) {
     uint32_t s = la.start;
     // in order from the true state: a segment whose guesses hold one is taken
     // whole; else it is re-run from the true state (exact for any DFA); an
-    // absorbing state ends the walk
-    for (uint64_t g = la.seg_off[i]; g < la.seg_off[i + 1] && s != la.matched && s != la.dead; ++g) {
+    // absorbing state ends the walk. A segment's guesses and exits do not
+    // depend on s: the next segment's are loaded while this one is decided, so
+    // the walk pays one memory latency per segment, not one per guess read.
+    const uint64_t g0 = la.seg_off[i], ge = la.seg_off[i + 1];
+    uint32_t gv[kLongGuesses], xv[kLongGuesses];
+    auto load = [&](uint64_t g, uint32_t(&gq)[kLongGuesses], uint32_t(&xq)[kLongGuesses]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < kLongGuesses; ++k) {
+        gq[k] = la.seg_guess[uint64_t(k) * la.nseg + g];
+        xq[k] = la.seg_exit[uint64_t(k) * la.nseg + g];
+      }
+    };
+    if (g0 < ge) load(g0, gv, xv);
+    for (uint64_t g = g0; g < ge && s != la.matched && s != la.dead; ++g) {
+      uint32_t gn[kLongGuesses], xn[kLongGuesses];
+      load(min(g + 1, ge - 1), gn, xn);
       uint32_t x = kNoGuess;
 #pragma unroll
-      for (int k = 0; k < kLongGuesses; ++k)
-        if (x == kNoGuess && la.seg_guess[uint64_t(k) * la.nseg + g] == s) x = la.seg_exit[uint64_t(k) * la.nseg + g];
+      for (int k = 0; k < kLongGuesses; ++k) x = (x == kNoGuess && gv[k] == s) ? xv[k] : x;
+#pragma unroll
+      for (int k = 0; k < kLongGuesses; ++k) {
+        gv[k] = gn[k];
+        xv[k] = xn[k];
+      }
       if (x != kNoGuess) {
         s = x;
       } else {

@@ -254,7 +254,7 @@ int grow(dgrep_ctx* c, T** p, uint64_t* cap, uint64_t need) {
 #define DGREP_SYNC_SPIN_US 1000
 #endif
 
-// The LDS image through which long_dfa_seg_kernel and verify_kernel read a
+// The LDS image through which long_dfa_seg1_kernel and verify_kernel read a
 // whole u16 DFA F ([S][K], breadth-first ids) with no HBM access on the chain:
 // rows [0, H) whole; then one DfaXRec (scan_common.h) for each state in
 // [H, S) -- its default = the resident row differing from its own in the

@@ -19,6 +19,6 @@ $HIPCC $FLAGS -c "$W/distributed-grep_amd/csrc/runtime/dgrep_runtime.hip" -o "$P
 wait %1 && wait %2
 $HIPCC -shared -fPIC --offload-arch=gfx950 -o "$P/variants/libdgrep_$NAME.so" "$P"/build/go_parser.o "$P"/build/dfa_builder.o \
   "$P"/build/compile_api.o "$P/build/scan_dfa_c_$NAME.o" "$P"/build/encode.o "$P"/build/reduce.o "$P/build/dgrep_runtime_c_$NAME.o" \
-  "$P"/build/build_info.o
+  "$P"/build/exchange.o "$P"/build/build_info.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 git -C "$R" worktree remove --force "$W"
 echo "built $NAME from $COMMIT"
