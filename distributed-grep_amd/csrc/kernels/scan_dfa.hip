@@ -97,9 +97,9 @@
 #ifndef DGREP_TABLE_WAVES
 #define DGREP_TABLE_WAVES 3
 #endif
-// Pair (C3, 20 states): one chunk per lane, runtime (adaptive) chunk from 4 KiB
+// Pair (C3, 20 states): one chunk per lane, runtime (adaptive) chunk from 3.5 KiB
 #ifndef DGREP_PAIR_CHUNK
-#define DGREP_PAIR_CHUNK 4096
+#define DGREP_PAIR_CHUNK 3584
 #endif
 #ifndef DGREP_PAIR_SLOTS
 #define DGREP_PAIR_SLOTS 16
@@ -2721,14 +2721,18 @@ hipError_t occ_t(int* b) {
 #endif
 constexpr uint64_t kShengMaxChunk = DGREP_SHENG_MAX_CHUNK;
 static_assert(kShengMaxChunk <= uint64_t(kMaxLaneChunk), "adaptive chunk above the slot limit");
-// Per-stepper ceiling: the pair stepper stops at 8 KiB. Round 2 (static
-// tiles) measured 8 KiB 4.43 ms, 16 KiB 4.39, 32 KiB 4.71 per 16 GiB (at 32
-// KiB most of its ~40 records per lane and tile go through the HBM spill
-// area); with tiles claimed dynamically, 8 KiB was at least as fast as 16 KiB
-// on each of three boxes (+0.3 %, +2.5 %, and +7 % against a slow mode 16 KiB
-// fell into in 1 of 6 runs on the first; profiles/r04/ablation/c3_chunk*.txt).
+// Per-stepper ceiling: the pair stepper stops at 7 KiB (3.5 KiB doubled once).
+// Round 2 (static tiles) measured 8 KiB 4.43 ms, 16 KiB 4.39, 32 KiB 4.71 per
+// 16 GiB (at 32 KiB most of its ~40 records per lane and tile go through the
+// HBM spill area); with tiles claimed dynamically, 8 KiB was at least as fast
+// as 16 KiB on each of three boxes (profiles/r04/ablation/c3_chunk*.txt).
+// Round 6, same box: 7 KiB (and 9 KiB) beat the power of two between them by
+// 2.5-3.5 % on two boxes (C3 kernel 0.567-0.575 -> 0.586-0.588), where the bare
+// access pattern (tools/pattern_ceiling) reads all three at one rate: a
+// 2^13-byte stride between a wave's lane streams costs the latency-bound pair
+// kernel, not the memory (profiles/r06/ablation/pair_chunk_*).
 #ifndef DGREP_PAIR_MAX_CHUNK
-#define DGREP_PAIR_MAX_CHUNK 8192
+#define DGREP_PAIR_MAX_CHUNK 7168
 #endif
 // Doubling also stops below DGREP_MIN_TILES_X2 / 2 tiles per resident wave
 // (Sheng, pair; the filter keeps 1):
