@@ -610,7 +610,6 @@ struct Blk {
   bool past;        // block lies at or beyond the chunk end
   uint32_t nlrun;   // '\n' consumed by the lane so far (r.nl at block start + this block's)
   uint32_t lnl;     // the line the next byte belongs to, encoded (lnl_update); 0: not owned
-  uint32_t evb;     // DGREP_EV_PROBE 2: event bits shifted in per word
 };
 // Where the current line started, as ONE register per block: lnl = 8 * (q + 3 +
 // kLnlOff) for the last '\n' seen at block offset q. Word J with newline mask m
@@ -826,27 +825,10 @@ __device__ __forceinline__ void word_nl(uint32_t m, Blk& b) {
 #ifndef DGREP_EV_BALLOT
 #define DGREP_EV_BALLOT ((1 << kStepPair) | (1 << kStepFilter))
 #endif
-#ifndef DGREP_EV_PROBE
-#define DGREP_EV_PROBE 0
-#endif
 template <int J, class Step, int E, bool DIRECT>
 __device__ __forceinline__ void word_events(const Step& st, uint32_t M, uint32_t m, uint32_t s0, uint32_t s1,
                                             uint32_t s2, uint32_t s3, Blk& b, LaneRun& r,
                                             const Emitter<E, DIRECT>& emit) {
-  if constexpr (DGREP_EV_PROBE != 0 && Step::kKind == kStepPair && !DIRECT) {
-    // timing probes (wrong output): 1 no event test, 2 event bits shifted in
-    // without a branch, 3 neither events nor newline bookkeeping, 4 the ballot
-    // branch with a one-instruction body
-    if constexpr (DGREP_EV_PROBE == 2) b.evb = b.evb + b.evb + (word_any(st, M, s0, s1, s2, s3) ? 1u : 0u);
-    if constexpr (DGREP_EV_PROBE == 4) {
-      const bool ev = word_any(st, M, s0, s1, s2, s3);
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
-        if (ev) asm volatile("v_add_u32 %0, 1, %0" : "+v"(b.evb));
-      }
-    }
-    if constexpr (DGREP_EV_PROBE != 3) word_nl<J>(m, b);
-    return;
-  }
   const bool ev = word_any(st, M, s0, s1, s2, s3);
   if constexpr (((DGREP_EV_BALLOT) >> Step::kKind) & 1) {
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
@@ -927,7 +909,6 @@ __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const
   b.pos = pos;
   b.past = pos >= C;
   b.nlrun = r.nl;
-  b.evb = 0;
   // inside the chunk: r.prev_nl - pos >= -(C + 1) > -kLnlOff
   if constexpr (SENT)
     b.lnl = !r.seen ? 0u : b.past ? kLnlSeen : 8u * uint32_t(int32_t(r.prev_nl - int64_t(pos)) + int32_t(3u + kLnlOff));
@@ -936,7 +917,6 @@ __device__ __forceinline__ void blk_init(Blk& b, uint64_t pos, uint64_t C, const
 }
 
 __device__ __forceinline__ void blk_finish(const Blk& b, uint32_t s, LaneRun& r) {
-  if constexpr (DGREP_EV_PROBE == 2 || DGREP_EV_PROBE == 4) asm volatile("" ::"v"(b.evb));
   r.s = s;
   r.nl = b.nlrun;
   if (b.lnl >= kLnlBase) {
@@ -2374,9 +2354,6 @@ constexpr uint32_t kLongDfaLdsBytes = 158 * 1024;  // rows + DfaXRec (u16 DFAs)
 #define DGREP_SEG_PIECES 4
 #endif
 constexpr int kSegPieces = DGREP_SEG_PIECES;
-#ifndef DGREP_SEG_CLS8
-#define DGREP_SEG_CLS8 1
-#endif
 template <typename E, bool XI>
 __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaArgs la) {
   __shared__ uint32_t cls[256];
@@ -2387,12 +2364,12 @@ __global__ __launch_bounds__(kLongDfaThreads) void long_dfa_seg1_kernel(LongDfaA
     cls[threadIdx.x] = uint32_t(la.cls[threadIdx.x]) * uint32_t(sizeof(E));
     cls8[threadIdx.x] = uint8_t(la.cls[threadIdx.x]);
   }
-  // a byte's scaled class. CLS8: from the u8 copy -- bytes b and b + 128 share
-  // a bank, so ASCII text reads it conflict-free (the u32 table's bank is b % 32:
-  // 'a', 'A' and '!' collide) -- for one more VALU op per byte
+  // a byte's scaled class, from the u8 copy: bytes b and b + 128 share a bank,
+  // so ASCII text reads it conflict-free (the u32 table's bank is b % 32: 'a',
+  // 'A' and '!' collide), for one more VALU op per byte (long_c4p +3.7 %,
+  // long_c4 unchanged, profiles/r06/long_ab/cls8_*)
   auto cl = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {
-    if constexpr (DGREP_SEG_CLS8) return uint32_t(cls8[b]) * uint32_t(sizeof(E));
-    return cls[b];
+    return uint32_t(cls8[b]) * uint32_t(sizeof(E));
   };
   E* const hot = reinterpret_cast<E*>(lbuf);
   const uint32_t hot_n = XI ? la.x_hot * la.nclasses : min(la.seg_hot_entries, uint32_t(kLongDfaHotBytes / sizeof(E)));
