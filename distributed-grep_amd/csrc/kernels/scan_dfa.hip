@@ -2717,10 +2717,12 @@ static_assert(kShengMaxChunk <= uint64_t(kMaxLaneChunk), "adaptive chunk above t
 // slower than 4 tiles of half the chunk (12 GiB: 32 KiB 4,462-4,580 GB/s,
 // 16 KiB 5,152), while 2.67 (16 GiB) and 5.33 (32 GiB) tiles per wave at
 // 32 KiB beat 16 KiB (profiles/r04/ablation/chunk_dyn.txt).
-// The filter stops at 32 KiB (64 KiB chunks were measured on the Sheng
-// stepper's access pattern only).
+// The filter stops at 64 KiB (one tile per resident wave on a 16 GiB split):
+// same box, C4 0.499-0.500 at 32 KiB -> 0.505-0.506 at 64 KiB, verification
+// 0.18 -> 0.16 ms (profiles/r06/ablation/filter_chunk_64k_c4_boxJ.txt), where
+// the Sheng stepper loses 6 % at 64 KiB (sheng_chunk_64k_c2_boxJ.txt).
 #ifndef DGREP_FILTER_MAX_CHUNK
-#define DGREP_FILTER_MAX_CHUNK 32768
+#define DGREP_FILTER_MAX_CHUNK 65536
 #endif
 #ifndef DGREP_MIN_TILES_X2
 #define DGREP_MIN_TILES_X2 5
