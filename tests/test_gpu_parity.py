@@ -493,19 +493,27 @@ def dgrep_unsupported():
     return dgrep.UnsupportedPattern
 
 
-def test_filter_candidates_dense_and_long(filter_ctx):
+@pytest.mark.parametrize("chunk", [0, 65536])  # 65536: the adaptive filter cap on 16 GiB splits
+def test_filter_candidates_dense_and_long(filter_ctx, chunk):
     """Every line a candidate (3 LDS rows): staging grows past the caller's
     capacity, verification keeps exactly the matching lines, at chunk, tile
     and overflow edges; lines longer than a chunk."""
     import dgrep
 
     filter_ctx.set_stepper("filter", 4)
-    for pattern in (b"error", b"(WARN|ERROR) [a-z_]+", b"^$|ab x"):
-        for data in (_dense_lines(5, 60000, 6), _dense_lines(6, 3000, 3000),
-                     dgrep.synth_corpus_host(3 << 20, 9, 0)):
-            _check(filter_ctx, pattern, data, threads=16)
-            st = filter_ctx.scan_stats()
-            assert st["stepper"] == "filter", st
+    big = (9 << 20) + 12345 if chunk else 3 << 20  # > 2 tiles at 64 KiB chunks
+    try:
+        filter_ctx.set_lane_chunk(chunk)
+        for pattern in (b"error", b"(WARN|ERROR) [a-z_]+", b"^$|ab x"):
+            for data in (_dense_lines(5, 60000, 6), _dense_lines(6, 3000, 3000),
+                         dgrep.synth_corpus_host(big, 9, 0)):
+                _check(filter_ctx, pattern, data, threads=16)
+                st = filter_ctx.scan_stats()
+                assert st["stepper"] == "filter", st
+                if chunk:
+                    assert st["lane_chunk"] == chunk, st
+    finally:
+        filter_ctx.set_lane_chunk(0)
 
 
 def test_filter_long_candidates_wave_verified(filter_ctx):
