@@ -97,9 +97,9 @@
 #ifndef DGREP_TABLE_WAVES
 #define DGREP_TABLE_WAVES 3
 #endif
-// Pair (C3, 20 states): one chunk per lane, runtime (adaptive) chunk from 3.5 KiB
+// Pair (C3, 20 states): one chunk per lane, runtime (adaptive) chunk from 4.5 KiB
 #ifndef DGREP_PAIR_CHUNK
-#define DGREP_PAIR_CHUNK 3584
+#define DGREP_PAIR_CHUNK 4608
 #endif
 #ifndef DGREP_PAIR_SLOTS
 #define DGREP_PAIR_SLOTS 16
@@ -2698,7 +2698,7 @@ hipError_t occ_t(int* b) {
 #endif
 constexpr uint64_t kShengMaxChunk = DGREP_SHENG_MAX_CHUNK;
 static_assert(kShengMaxChunk <= uint64_t(kMaxLaneChunk), "adaptive chunk above the slot limit");
-// Per-stepper ceiling: the pair stepper stops at 7 KiB (3.5 KiB doubled once).
+// Per-stepper ceiling: the pair stepper stops at 9 KiB (4.5 KiB doubled once).
 // Round 2 (static tiles) measured 8 KiB 4.43 ms, 16 KiB 4.39, 32 KiB 4.71 per
 // 16 GiB (at 32 KiB most of its ~40 records per lane and tile go through the
 // HBM spill area); with tiles claimed dynamically, 8 KiB was at least as fast
@@ -2707,9 +2707,12 @@ static_assert(kShengMaxChunk <= uint64_t(kMaxLaneChunk), "adaptive chunk above t
 // 2.5-3.5 % on two boxes (C3 kernel 0.567-0.575 -> 0.586-0.588), where the bare
 // access pattern (tools/pattern_ceiling) reads all three at one rate: a
 // 2^13-byte stride between a wave's lane streams costs the latency-bound pair
-// kernel, not the memory (profiles/r06/ablation/pair_chunk_*).
+// kernel, not the memory (profiles/r06/ablation/pair_chunk_*). 9 KiB runs at
+// least as fast as 7 KiB on every box tried (0-1 %; a fast box 0.633 -> 0.638,
+// pair_chunk_7k_vs_9k_c3_boxM.txt), and 4.5 KiB, the small-split floor, is the
+// best chunk of the bare access pattern (pattern_ceiling_sweep_pair_lds.txt).
 #ifndef DGREP_PAIR_MAX_CHUNK
-#define DGREP_PAIR_MAX_CHUNK 7168
+#define DGREP_PAIR_MAX_CHUNK 9216
 #endif
 // Doubling also stops below DGREP_MIN_TILES_X2 / 2 tiles per resident wave
 // (Sheng, pair; the filter keeps 1):

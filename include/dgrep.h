@@ -125,9 +125,9 @@ int dgrep_load_dfa(dgrep_ctx* ctx, const void* blob, size_t n);
 int dgrep_set_stepper(dgrep_ctx* ctx, int force, uint32_t filter_rows);
 /* Tests / tuning: lane chunk of the Sheng (<= 8-state), pair and filter
  * steppers for later scans. 0 (default) = adaptive: the compiled chunk (4 KiB;
- * pair 3.5 KiB), doubled while every resident wave still gets a tile and the
+ * pair 4.5 KiB), doubled while every resident wave still gets a tile and the
  * matching lines the previous scan's density predicts fill at most a quarter
- * of a lane's record capacity, up to 32 KiB (Sheng), 64 KiB (filter) or 7 KiB (pair). Otherwise a
+ * of a lane's record capacity, up to 32 KiB (Sheng), 64 KiB (filter) or 9 KiB (pair). Otherwise a
  * multiple of 128 in [4096, 65536] (the LDS slots hold 16-bit chunk offsets;
  * a line starting exactly at a 64 KiB chunk end is flagged separately);
  * anything else is DGREP_E_INVALID and leaves the setting unchanged. No effect

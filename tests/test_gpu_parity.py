@@ -310,13 +310,13 @@ def test_adaptive_chunk_on_large_split_and_density_cap(gpu_ctx):
     assert chunks[("error", 0)] >= 8192 and chunks[("error", 1)] == chunks[("error", 0)], chunks
     # "r" matches nearly every ~120-B line: 24 slots cap the chunk at the 4 KiB floor
     assert chunks[("r", 0)] >= 8192 and chunks[("r", 1)] == 4096, chunks
-    # the pair stepper (config 3's pattern): 3.5 KiB doubled once, to its 7 KiB cap
+    # the pair stepper (config 3's pattern): 4.5 KiB doubled once, to its 9 KiB cap
     c3 = "^[0-9]{4}-[0-9]{2}.*(WARN|ERROR) [a-z_]+"
     gpu_ctx.load(c3)
     cnt = gpu_ctx.scan_device(buf.data_ptr(), n, ln.data_ptr(), st.data_ptr(), le.data_ptr(), cap)
     assert 0 <= cnt <= cap
     s = gpu_ctx.scan_stats()
-    assert s["stepper"] == "pair" and s["lane_chunk"] == 7168, s
+    assert s["stepper"] == "pair" and s["lane_chunk"] == 9216, s
     assert bench.verify_windows(buf, n, ln[:cnt], st[:cnt], le[:cnt], c3, 3, 1 << 20) == 3
     del buf, ln, st, le
     torch.cuda.empty_cache()
